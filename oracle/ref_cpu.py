@@ -1,0 +1,208 @@
+"""Torch-CPU restatement of the reference hot path -- TEST INFRASTRUCTURE ONLY.
+
+Written from the reference's behaviour, functionally (a parameter dict keyed by
+the reference's state_dict names), so the same arithmetic can be replayed on
+the CPU next to the HIP path.  Every function cites the reference lines it
+restates.  Pinned by tests/test_oracle.py against tests/golden/*.npz, which
+were produced by importing the reference itself (tools/gen_golden.py).
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+
+def _t(x, dtype=torch.float32):
+    if isinstance(x, torch.Tensor):
+        return x
+    return torch.as_tensor(np.asarray(x), dtype=dtype)
+
+
+# ---------------------------------------------------------------- geometry
+def get_rays(H, W, focal, c2w):
+    """src/utils.py:10-19.  Pixel (row j, col i) -> OpenGL camera ray.
+
+    ``focal`` may be a python float or a float64 tensor of shape (1,) (what
+    default_collate makes of the float focal, src/data.py:31-37); in the
+    latter case the camera-space directions are formed in float64 and only
+    then cast to c2w's dtype, exactly as torch type promotion does in the
+    reference.  No +0.5 pixel-centre offset; principal point (W/2, H/2).
+    """
+    c2w = _t(c2w)
+    cols = torch.arange(W, dtype=torch.float32)   # == linspace(0, W-1, W)
+    rows = torch.arange(H, dtype=torch.float32)
+    jj, ii = torch.meshgrid(rows, cols, indexing="ij")   # (H, W)
+    f = focal if isinstance(focal, torch.Tensor) else torch.tensor(float(focal), dtype=torch.float32)
+    dx = (ii - W * 0.5) / f
+    dy = -(jj - H * 0.5) / f
+    cam = torch.stack([dx, dy, -torch.ones_like(dx)], -1).to(c2w.dtype)   # (H, W, 3)
+    R = c2w[:3, :3]
+    # world dir component a = sum_b cam[b] * R[a, b]  (three products, summed in order)
+    prods = cam[..., None, :] * R                       # (H, W, 3, 3)
+    d = torch.sum(prods, -1)
+    vd = d / torch.norm(d, dim=-1, keepdim=True)
+    ro = c2w[:3, 3].expand(d.shape)
+    return ro.reshape(-1, 3), vd.reshape(-1, 3)
+
+
+def stratified_z(near, far, n, jitter=None, z_fixed=False):
+    """src/utils.py:24-29.  One z vector shared by all rays.  ``jitter`` is the
+    (n,) U[0,1) draw the reference takes with torch.rand(n) (upper half-bin)."""
+    if z_fixed:
+        return torch.linspace(near, far, n)
+    half = (far - near) / (2 * n)
+    z = torch.linspace(near + half, far - half, n)
+    if jitter is None:
+        jitter = torch.rand(n)
+    return z + _t(jitter) * (far - near) / (2 * n)
+
+
+def sample_from_rays(ro, vd, near, far, n, jitter=None, z_fixed=False):
+    """src/utils.py:21-32 -> (xyz (R,n,3), viewdir (R,n,3), z (n,))."""
+    z = stratified_z(near, far, n, jitter, z_fixed).type_as(ro)
+    xyz = ro[:, None, :] + vd[:, None, :] * z[:, None]
+    return xyz, vd[:, None, :].expand(-1, n, -1).contiguous(), z
+
+
+# ---------------------------------------------------------------- model
+def positional_encoding(x, n_freq):
+    """src/model.py:4-7: [x, sin(2^i x)..., cos(2^i x)...], frequency-major,
+    component-minor, no pi."""
+    scaled = [x * (2.0 ** i) for i in range(n_freq)]
+    y = torch.cat(scaled, -1)
+    return torch.cat([x, torch.sin(y), torch.cos(y)], -1)
+
+
+def _lin(p, name, x):
+    return F.linear(x, p[name + ".weight"], p[name + ".bias"])
+
+
+def codenerf_forward(p, xyz, viewdir, shape_code, texture_code, shape_blocks=3,
+                     texture_blocks=1, num_xyz_freq=10, num_dir_freq=4, acts=None):
+    """src/model.py:36-53.  Returns (sigmas (...,1), rgbs (...,3)).
+
+    Latent injection: y <- y + ReLU(L_j code + c_j) before every shape /
+    texture layer; encoding_shape has no activation; sigma = Softplus(beta=1,
+    threshold=20); the rgb head is linear (no sigmoid).  ``acts`` (a dict)
+    optionally receives every intermediate for per-layer checks.
+    """
+    h = F.relu(_lin(p, "encoding_xyz.0", positional_encoding(xyz, num_xyz_freq)))
+    if acts is not None:
+        acts["y0"] = h
+    for j in range(1, shape_blocks + 1):
+        z = F.relu(_lin(p, f"shape_latent_layer_{j}.0", shape_code))
+        h = F.relu(_lin(p, f"shape_layer_{j}.0", h + z))
+        if acts is not None:
+            acts[f"y{j}"] = h
+    h = _lin(p, "encoding_shape", h)
+    if acts is not None:
+        acts["y_shape"] = h
+    sig = F.softplus(_lin(p, "sigma.0", h), beta=1.0, threshold=20.0)
+    h = F.relu(_lin(p, "encoding_viewdir.0",
+                    torch.cat([h, positional_encoding(viewdir, num_dir_freq)], -1)))
+    if acts is not None:
+        acts["y_view"] = h
+    for j in range(1, texture_blocks + 1):
+        z = F.relu(_lin(p, f"texture_latent_layer_{j}.0", texture_code))
+        h = F.relu(_lin(p, f"texture_layer_{j}.0", h + z))
+        if acts is not None:
+            acts[f"y_tex{j}"] = h
+    h = F.relu(_lin(p, "rgb.0", h))
+    if acts is not None:
+        acts["y_rgb0"] = h
+    return sig, _lin(p, "rgb.2", h)
+
+
+# ---------------------------------------------------------------- rendering
+def volume_rendering(sigmas, rgbs, z_vals, white_bg=True):
+    """src/utils.py:34-47.  Alpha compositing along the sample axis.
+
+    z_vals may be (N,) (shared, as the reference) or (R,N) (per ray, used by
+    the fine-sampling extension).  The last interval is 1e10; transmittance
+    is the exclusive cumulative product of (1 - alpha + 1e-10).
+    """
+    sig = sigmas[..., 0] if sigmas.dim() == 3 else sigmas
+    gaps = z_vals[..., 1:] - z_vals[..., :-1]
+    gaps = torch.cat([gaps, torch.full_like(gaps[..., :1], 1e10)], -1)
+    alpha = 1 - torch.exp(-sig * gaps)
+    keep = 1 - alpha + 1e-10
+    T = torch.cumprod(torch.cat([torch.ones_like(keep[..., :1]), keep], -1), -1)[..., :-1]
+    w = alpha * T
+    rgb = torch.sum(w[..., None] * rgbs, -2)
+    depth = torch.sum(w * z_vals, -1)
+    if white_bg:
+        rgb = rgb + 1 - w.sum(1)[..., None]
+    return rgb, depth
+
+
+# ---------------------------------------------------------------- training
+def param_tensors(np_params, requires_grad=True):
+    return {k: torch.tensor(v, requires_grad=requires_grad) for k, v in np_params.items()}
+
+
+def image_step(p, shape_table, texture_table, obj_idx, ro, vd, z_vals, gt, chunk=2048,
+               reg_coef=1e-4, net=None):
+    """One image of the training loop, src/trainer.py:65-84.
+
+    Chunks of ``chunk`` rays: per-chunk mean MSE, ``loss.backward()`` per
+    chunk (so gradients are the sum of chunk-mean gradients) and the code
+    regulariser ``reg_coef * mean(|s| + |t|)`` added on chunk 0 only.
+    ``p`` / tables must be leaf tensors with requires_grad; gradients are
+    accumulated into ``.grad``.  Returns (per-chunk l2 losses, rgb image).
+    """
+    net = net or {}
+    n = z_vals.shape[-1]
+    R = ro.shape[0]
+    losses, outs = [], []
+    for a in range(0, R, chunk):
+        b = min(a + chunk, R)
+        s = shape_table[obj_idx][None]
+        t = texture_table[obj_idx][None]
+        zc = z_vals if z_vals.dim() == 1 else z_vals[a:b]
+        xyz = ro[a:b, None, :] + vd[a:b, None, :] * zc[..., None]
+        vdir = vd[a:b, None, :].expand(-1, n, -1)
+        sig, rgbs = codenerf_forward(p, xyz, vdir, s, t, **net)
+        rgb, _ = volume_rendering(sig, rgbs, zc)
+        l2 = torch.mean((rgb - gt[a:b]) ** 2)
+        loss = l2
+        if a == 0:
+            loss = l2 + reg_coef * torch.mean(torch.norm(s, dim=-1) + torch.norm(t, dim=-1))
+        loss.backward()
+        losses.append(l2.item())
+        outs.append(rgb.detach())
+    return losses, torch.cat(outs)
+
+
+class AdamWRef:
+    """torch.optim.AdamW defaults as used at src/trainer.py:116-120
+    (betas 0.9/0.999, eps 1e-8, weight_decay 0.01, no amsgrad), restated in
+    the single-tensor update order so it can be mirrored elementwise."""
+
+    def __init__(self, groups, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
+        self.groups = groups          # [(list_of_tensors, lr)]
+        self.b1, self.b2 = betas
+        self.eps, self.wd = eps, weight_decay
+        self.state = {}
+
+    @torch.no_grad()
+    def step(self):
+        for params, lr in self.groups:
+            for p in params:
+                if p.grad is None:
+                    continue
+                st = self.state.setdefault(id(p), [0, torch.zeros_like(p), torch.zeros_like(p)])
+                st[0] += 1
+                step, m, v = st
+                p.mul_(1 - lr * self.wd)
+                m.lerp_(p.grad, 1 - self.b1)
+                v.mul_(self.b2).addcmul_(p.grad, p.grad, value=1 - self.b2)
+                bc1 = 1 - self.b1 ** step
+                bc2 = 1 - self.b2 ** step
+                denom = (v.sqrt() / math.sqrt(bc2)).add_(self.eps)
+                p.addcdiv_(m, denom, value=-(lr / bc1))
+
+
+def psnr(mse):
+    """src/trainer.py:99."""
+    return -10.0 * np.log(mse) / np.log(10.0)
