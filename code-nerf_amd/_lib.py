@@ -1,0 +1,102 @@
+"""ctypes binding of the C ABI in include/codenerf.h (libcodenerf_hip.so).
+
+This is the product path's only way to compute: if the library or a HIP device
+is missing, every entry point raises ``HipUnavailable`` -- there is no CPU
+fallback.  torch is imported first so the process already holds torch's HIP
+runtime (SONAME libamdhip64.so.7) when the library is loaded.
+"""
+import ctypes
+import os
+
+import torch
+
+LIB_NAME = "libcodenerf_hip.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+CN_FP32 = 0
+CN_BF16 = 1
+
+
+class HipUnavailable(RuntimeError):
+    pass
+
+
+class CnError(RuntimeError):
+    pass
+
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_F = ctypes.c_float
+_D = ctypes.c_double
+_Z = ctypes.c_size_t
+
+_SIGS = {
+    "cn_abi_version": (_I, []),
+    "cn_last_error": (ctypes.c_char_p, []),
+    "cn_plan_create": (_I, [_I, _I, _I, _I, _I, _I, _I, ctypes.POINTER(_P)]),
+    "cn_plan_destroy": (None, [_P]),
+    "cn_plan_num_params": (_I, [_P]),
+    "cn_plan_num_inject": (_I, [_P]),
+    "cn_pad_samples": (_I, [_P, _I]),
+    "cn_packed_bytes": (_Z, [_P, _I]),
+    "cn_blob_floats": (_Z, [_P]),
+    "cn_act_bytes": (_Z, [_P, _I]),
+    "cn_dw_ws_bytes": (_Z, [_P, _I]),
+    "cn_pack_weights": (_I, [_P, _P, _P, _P, _P]),
+    "cn_latent_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P]),
+    "cn_mlp_fwd": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P]),
+    "cn_mlp_bwd": (_I, [_P, _P, _P, _I, _P, _P, _P, _P]),
+    "cn_mlp_dw": (_I, [_P, _P, _I, _P, _P, _P, _P, _P]),
+    "cn_latent_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P]),
+    "cn_get_rays": (_I, [_I, _I, _D, _I, _P, _P, _P, _P]),
+    "cn_sample_points": (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P]),
+    "cn_composite_fwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P]),
+    "cn_composite_bwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
+    "cn_render_loss": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P]),
+    "cn_adamw_step": (_I, [_I, _P, _P, _P, _P, _P, _P, _D, _D, _D, _D, _I, _P]),
+}
+
+EXPORTED = tuple(_SIGS)
+_lib = None
+
+
+def load_library(path=LIB_PATH):
+    """Load and type the shared library (no device needed)."""
+    if not os.path.exists(path):
+        raise HipUnavailable(f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.cn_abi_version() != 1:
+        raise HipUnavailable("libcodenerf_hip.so ABI version mismatch")
+    return lib
+
+
+def lib():
+    """The loaded library; requires a visible HIP device."""
+    global _lib
+    if _lib is None:
+        if not torch.cuda.is_available():
+            raise HipUnavailable("no HIP device visible: the CodeNeRF MI355X path has no CPU fallback")
+        _lib = load_library()
+    return _lib
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = lib().cn_last_error().decode(errors="replace")
+        raise CnError(f"{what}: {msg}" if what else msg)
+
+
+def ptr(t):
+    """Device pointer of a tensor (or None -> NULL)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_ptr(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

@@ -1,0 +1,294 @@
+// C ABI of the CodeNeRF gfx950 hot path (include/codenerf.h).
+#include <stdio.h>
+#include <string.h>
+#include <algorithm>
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "../../include/codenerf.h"
+#include "chain_inst.h"
+#include "latent_args.h"
+#include "dw.hip"
+#include "optim.hip"
+#include "render.hip"
+
+using namespace cn;
+
+struct cn_plan {
+  ChainSet cs;
+  int32_t* d_fwd_idx = nullptr;
+  int32_t* d_bwd_idx = nullptr;
+  int fwd_n = 0, bwd_n = 0;
+};
+
+namespace {
+thread_local std::string g_err;
+
+int fail(const std::string& msg) {
+  g_err = msg;
+  return -1;
+}
+int check(hipError_t e, const char* what) {
+  if (e != hipSuccess) return fail(std::string(what) + ": " + hipGetErrorString(e));
+  return 0;
+}
+int launch_check(const char* what) { return check(hipGetLastError(), what); }
+hipStream_t S(void* s) { return (hipStream_t)s; }
+int grid_for(long n, int per) { return (int)((n + per - 1) / per); }
+}  // namespace
+
+extern "C" {
+
+int cn_abi_version(void) { return CN_ABI_VERSION; }
+const char* cn_last_error(void) { return g_err.c_str(); }
+
+int cn_plan_create(int shape_blocks, int texture_blocks, int W, int num_xyz_freq, int num_dir_freq,
+                   int latent_dim, int precision, cn_plan** out) {
+  if (!out) return fail("cn_plan_create: out is NULL");
+  *out = nullptr;
+  if (W != 256 || latent_dim != 256 || num_xyz_freq != 10 || num_dir_freq != 4)
+    return fail("cn_plan_create: unsupported net (need W=latent_dim=256, num_xyz_freq=10, num_dir_freq=4)");
+  if (precision != CN_FP32 && precision != CN_BF16) return fail("cn_plan_create: precision must be CN_FP32 or CN_BF16");
+  ChainSet cs;
+  if (shape_blocks == 3 && texture_blocks == 1) cs = precision ? chain_set_bf16_3_1() : chain_set_fp32_3_1();
+  else if (shape_blocks == 2 && texture_blocks == 1) cs = precision ? chain_set_bf16_2_1() : chain_set_fp32_2_1();
+  else return fail("cn_plan_create: unsupported (shape_blocks, texture_blocks); built: (3,1), (2,1)");
+  cn_plan* p = new cn_plan();
+  p->cs = cs;
+  std::vector<int32_t> tf = cs.fwd_table(), tb = cs.bwd_table();
+  p->fwd_n = (int)tf.size();
+  p->bwd_n = (int)tb.size();
+  if (check(hipMalloc(&p->d_fwd_idx, tf.size() * 4), "hipMalloc") ||
+      check(hipMalloc(&p->d_bwd_idx, tb.size() * 4), "hipMalloc") ||
+      check(hipMemcpy(p->d_fwd_idx, tf.data(), tf.size() * 4, hipMemcpyHostToDevice), "hipMemcpy") ||
+      check(hipMemcpy(p->d_bwd_idx, tb.data(), tb.size() * 4, hipMemcpyHostToDevice), "hipMemcpy")) {
+    std::string e = g_err;
+    cn_plan_destroy(p);
+    return fail(e);
+  }
+  *out = p;
+  return 0;
+}
+
+void cn_plan_destroy(cn_plan* p) {
+  if (!p) return;
+  if (p->d_fwd_idx) (void)hipFree(p->d_fwd_idx);
+  if (p->d_bwd_idx) (void)hipFree(p->d_bwd_idx);
+  delete p;
+}
+
+int cn_plan_num_params(const cn_plan* p) { return p ? p->cs.n_params : -1; }
+int cn_plan_num_inject(const cn_plan* p) { return p ? p->cs.n_inject : -1; }
+int cn_pad_samples(const cn_plan* p, int M) { return p ? ((M + 255) / 256) * 256 : -1; }
+size_t cn_packed_bytes(const cn_plan* p, int bwd) { return p ? (bwd ? p->cs.pack_bwd_bytes : p->cs.pack_fwd_bytes) : 0; }
+size_t cn_blob_floats(const cn_plan* p) { return p ? (size_t)p->cs.blob_floats : 0; }
+size_t cn_act_bytes(const cn_plan* p, int M) { return p ? p->cs.layout(cn_pad_samples(p, M)).bytes : 0; }
+size_t cn_dw_ws_bytes(const cn_plan* p, int M) { return p ? p->cs.dw_ws_bytes(M) : 0; }
+
+int cn_pack_weights(const cn_plan* p, const float* const* d_params, void* d_fwd, void* d_bwd, void* stream) {
+  if (!p || !d_params) return fail("cn_pack_weights: NULL argument");
+  const int bf16 = p->cs.prec;
+  if (d_fwd) {
+    hipLaunchKernelGGL(pack_kernel, dim3(grid_for(p->fwd_n, 256)), dim3(256), 0, S(stream), d_params,
+                       p->d_fwd_idx, p->fwd_n, d_fwd, bf16);
+    if (launch_check("pack_kernel(fwd)")) return -1;
+  }
+  if (d_bwd) {
+    hipLaunchKernelGGL(pack_kernel, dim3(grid_for(p->bwd_n, 256)), dim3(256), 0, S(stream), d_params,
+                       p->d_bwd_idx, p->bwd_n, d_bwd, bf16);
+    if (launch_check("pack_kernel(bwd)")) return -1;
+  }
+  return 0;
+}
+
+int cn_latent_fwd(const cn_plan* p, const float* const* d_params, const float* d_shape, const float* d_tex,
+                  float* d_blob, float* d_zvec, void* stream) {
+  if (!p || !d_params || !d_shape || !d_tex || !d_blob || !d_zvec) return fail("cn_latent_fwd: NULL argument");
+  LatentArgs a{d_params, d_shape, d_tex, d_blob, d_zvec};
+  hipLaunchKernelGGL(p->cs.latent_fwd, dim3(p->cs.n_fwd_layers + 1), dim3(256), 0, S(stream), a);
+  return launch_check("latent_fwd_kernel");
+}
+
+int cn_mlp_fwd(const cn_plan* p, const void* d_pack, const float* d_blob, int M, const float* d_xyz,
+               const float* d_viewdir, const float* d_rays_o, const float* d_rays_d, const float* d_z,
+               int z_stride, int n_samples, float* d_sigma, float* d_rgb, void* d_act, void* stream) {
+  if (!p || !d_pack || !d_blob || !d_sigma || !d_rgb) return fail("cn_mlp_fwd: NULL argument");
+  if (M <= 0) return fail("cn_mlp_fwd: M must be positive");
+  ChainArgs a{};
+  a.wpack = d_pack;
+  a.bias = d_blob;
+  a.M = M;
+  if (d_xyz) {
+    if (!d_viewdir) return fail("cn_mlp_fwd: xyz given without viewdir");
+    a.mode = 0;
+    a.xyz = d_xyz;
+    a.vdir = d_viewdir;
+    a.nsamp = 1;
+  } else {
+    if (!d_rays_o || !d_rays_d || !d_z || n_samples <= 0) return fail("cn_mlp_fwd: ray mode needs rays_o, rays_d, z, n_samples");
+    if (M % n_samples) return fail("cn_mlp_fwd: M must be a multiple of n_samples in ray mode");
+    if (z_stride != 0 && z_stride != n_samples) return fail("cn_mlp_fwd: z_stride must be 0 or n_samples");
+    a.mode = 1;
+    a.rays_o = d_rays_o;
+    a.rays_d = d_rays_d;
+    a.zvals = d_z;
+    a.z_stride = z_stride;
+    a.nsamp = n_samples;
+  }
+  a.sigma = d_sigma;
+  a.rgb = d_rgb;
+  const int Mp = cn_pad_samples(p, M);
+  if (d_act) {
+    const ActLayout L = p->cs.layout(Mp);
+    char* b = (char*)d_act;
+    a.pe = b + L.pe;
+    a.dir = b + L.dir;
+    for (int i = 0; i < kMaxPlanes; ++i) { a.Y[i] = b + L.Y[i]; a.dA[i] = b + L.dA[i]; }
+    a.d8 = b + L.d8;
+    a.spre = (float*)(b + L.spre);
+    a.masks = (uint32_t*)(b + L.masks);
+  }
+  const int grid = Mp / p->cs.tile;
+  hipLaunchKernelGGL(d_act ? p->cs.fwd_train : p->cs.fwd_infer, dim3(grid), dim3(p->cs.waves * 64), 0,
+                     S(stream), a);
+  return launch_check("chain_kernel(fwd)");
+}
+
+int cn_mlp_bwd(const cn_plan* p, const void* d_pack, const float* d_blob, int M, const float* d_dsigma,
+               const float* d_drgb, void* d_act, void* stream) {
+  if (!p || !d_pack || !d_blob || !d_dsigma || !d_drgb || !d_act) return fail("cn_mlp_bwd: NULL argument");
+  if (M <= 0) return fail("cn_mlp_bwd: M must be positive");
+  ChainArgs a{};
+  a.wpack = d_pack;
+  a.bias = d_blob;
+  a.M = M;
+  a.dsigma = d_dsigma;
+  a.drgb = d_drgb;
+  const int Mp = cn_pad_samples(p, M);
+  const ActLayout L = p->cs.layout(Mp);
+  char* b = (char*)d_act;
+  a.pe = b + L.pe;
+  a.dir = b + L.dir;
+  for (int i = 0; i < kMaxPlanes; ++i) { a.Y[i] = b + L.Y[i]; a.dA[i] = b + L.dA[i]; }
+  a.d8 = b + L.d8;
+  a.spre = (float*)(b + L.spre);
+  a.masks = (uint32_t*)(b + L.masks);
+  hipLaunchKernelGGL(p->cs.bwd, dim3(Mp / p->cs.tile), dim3(p->cs.waves * 64), 0, S(stream), a);
+  return launch_check("chain_kernel(bwd)");
+}
+
+int cn_mlp_dw(const cn_plan* p, void* d_act, int M, const float* d_zvec, float* const* d_grads, float* d_dbuf,
+              void* d_ws, void* stream) {
+  if (!p || !d_act || !d_zvec || !d_grads || !d_dbuf || !d_ws) return fail("cn_mlp_dw: NULL argument");
+  if (M <= 0) return fail("cn_mlp_dw: M must be positive");
+  DwArgs dw;
+  DwRedArgs red;
+  const int nwg = p->cs.dw_setup((char*)d_act, M, d_zvec, d_dbuf, (char*)d_ws, &dw, &red);
+  red.grads = d_grads;
+  if (p->cs.prec) hipLaunchKernelGGL(dw_kernel<CN_P_BF16>, dim3(nwg), dim3(256), 0, S(stream), dw);
+  else hipLaunchKernelGGL(dw_kernel<CN_P_FP32>, dim3(nwg), dim3(256), 0, S(stream), dw);
+  if (launch_check("dw_kernel")) return -1;
+  hipLaunchKernelGGL(dw_reduce_kernel, dim3(grid_for(red.prefix[red.nprob], 256)), dim3(256), 0, S(stream), red);
+  return launch_check("dw_reduce_kernel");
+}
+
+int cn_latent_bwd(const cn_plan* p, const float* const* d_params, float* const* d_grads, const float* d_shape,
+                  const float* d_tex, const float* d_zvec, const float* d_dbuf, float* d_scratch, float* d_dshape,
+                  float* d_dtex, float reg_coef, float* d_reg_out, void* stream) {
+  if (!p || !d_params || !d_grads || !d_shape || !d_tex || !d_zvec || !d_dbuf || !d_scratch || !d_dshape || !d_dtex)
+    return fail("cn_latent_bwd: NULL argument");
+  LatentBwdArgs a{d_params, d_grads, d_shape, d_tex, d_zvec, d_dbuf, d_scratch, d_dshape, d_dtex, reg_coef, d_reg_out};
+  hipLaunchKernelGGL(p->cs.latent_bwd, dim3(p->cs.n_inject), dim3(256), 0, S(stream), a);
+  if (launch_check("latent_bwd_kernel")) return -1;
+  hipLaunchKernelGGL(p->cs.code_grad, dim3(2), dim3(256), 0, S(stream), a);
+  return launch_check("code_grad_kernel");
+}
+
+int cn_get_rays(int H, int W, double focal, int focal_is_f64, const float* d_c2w, float* d_ro, float* d_vd,
+                void* stream) {
+  if (!d_c2w || !d_ro || !d_vd || H <= 0 || W <= 0) return fail("cn_get_rays: bad argument");
+  hipLaunchKernelGGL(get_rays_kernel, dim3(grid_for((long)H * W, 256)), dim3(256), 0, S(stream), H, W, focal,
+                     focal_is_f64, d_c2w, d_ro, d_vd);
+  return launch_check("get_rays_kernel");
+}
+
+int cn_sample_points(const float* d_ro, const float* d_vd, const float* d_z, int z_stride, int R, int N,
+                     float* d_xyz, float* d_vrep, void* stream) {
+  if (!d_ro || !d_vd || !d_z || !d_xyz || !d_vrep || R <= 0 || N <= 0) return fail("cn_sample_points: bad argument");
+  hipLaunchKernelGGL(stratified_points_kernel, dim3(grid_for((long)R * N, 256)), dim3(256), 0, S(stream), d_ro,
+                     d_vd, d_z, z_stride, R, N, d_xyz, d_vrep);
+  return launch_check("stratified_points_kernel");
+}
+
+static int check_rn(int R, int N, const char* who) {
+  if (R <= 0 || N <= 0) return fail(std::string(who) + ": R and N must be positive");
+  if (N > 64 * kMaxPer) return fail(std::string(who) + ": at most 256 samples per ray");
+  return 0;
+}
+
+int cn_composite_fwd(const float* d_sigma, const float* d_rgb, const float* d_z, int z_stride, int R, int N,
+                     int white_bg, float* d_out_rgb, float* d_out_depth, float* d_w, void* stream) {
+  if (!d_sigma || !d_rgb || !d_z || !d_out_rgb || !d_out_depth) return fail("cn_composite_fwd: NULL argument");
+  if (check_rn(R, N, "cn_composite_fwd")) return -1;
+  hipLaunchKernelGGL(composite_fwd_kernel, dim3(grid_for(R, 4)), dim3(256), 0, S(stream), d_sigma, d_rgb, d_z,
+                     z_stride, R, N, white_bg, d_out_rgb, d_out_depth, d_w);
+  return launch_check("composite_fwd_kernel");
+}
+
+int cn_composite_bwd(const float* d_sigma, const float* d_rgb, const float* d_z, int z_stride, int R, int N,
+                     int white_bg, const float* d_grgb, const float* d_gdepth, float* d_dsig, float* d_drgb,
+                     void* stream) {
+  if (!d_sigma || !d_rgb || !d_z || !d_grgb || !d_dsig || !d_drgb) return fail("cn_composite_bwd: NULL argument");
+  if (check_rn(R, N, "cn_composite_bwd")) return -1;
+  hipLaunchKernelGGL(composite_bwd_kernel, dim3(grid_for(R, 4)), dim3(256), 0, S(stream), d_sigma, d_rgb, d_z,
+                     z_stride, R, N, white_bg, d_grgb, d_gdepth, d_dsig, d_drgb);
+  return launch_check("composite_bwd_kernel");
+}
+
+int cn_render_loss(const float* d_sigma, const float* d_rgb, const float* d_z, int z_stride, int R, int N,
+                   int white_bg, const float* d_gt, int chunk, float* d_out_rgb, float* d_ray_se,
+                   float* d_chunk_loss, float* d_dsig, float* d_drgb, void* stream) {
+  if (!d_sigma || !d_rgb || !d_z || !d_gt || !d_out_rgb || !d_ray_se || !d_chunk_loss || !d_dsig || !d_drgb)
+    return fail("cn_render_loss: NULL argument");
+  if (check_rn(R, N, "cn_render_loss")) return -1;
+  if (chunk <= 0) return fail("cn_render_loss: chunk must be positive");
+  hipLaunchKernelGGL(render_loss_kernel, dim3(grid_for(R, 4)), dim3(256), 0, S(stream), d_sigma, d_rgb, d_z,
+                     z_stride, R, N, white_bg, d_gt, chunk, d_out_rgb, d_ray_se, d_dsig, d_drgb);
+  if (launch_check("render_loss_kernel")) return -1;
+  hipLaunchKernelGGL(chunk_loss_kernel, dim3(grid_for(R, chunk)), dim3(256), 0, S(stream), d_ray_se, R, chunk,
+                     d_chunk_loss);
+  return launch_check("chunk_loss_kernel");
+}
+
+int cn_adamw_step(int nseg, float* const* p, const float* const* g, float* const* m, float* const* v,
+                  const int* n, const double* lr, double wd, double beta1, double beta2, double eps, int step,
+                  void* stream) {
+  if (nseg <= 0 || !p || !g || !m || !v || !n || !lr) return fail("cn_adamw_step: bad argument");
+  if (step < 1) return fail("cn_adamw_step: step must be >= 1");
+  const double bc1 = 1.0 - std::pow(beta1, step);
+  const double bc2 = 1.0 - std::pow(beta2, step);
+  for (int base = 0; base < nseg; base += kAdamMaxSeg) {
+    AdamArgs a{};
+    a.nseg = std::min(kAdamMaxSeg, nseg - base);
+    long total = 0;
+    for (int i = 0; i < a.nseg; ++i) {
+      const int k = base + i;
+      a.s[i] = AdamSeg{p[k], g[k], m[k], v[k], n[k], (float)(1.0 - lr[k] * wd), (float)(-(lr[k] / bc1))};
+      a.prefix[i] = (int)total;
+      total += n[k];
+    }
+    a.prefix[a.nseg] = (int)total;
+    a.lerp_w = (float)(1.0 - beta1);
+    a.beta2 = (float)beta2;
+    a.one_m_beta2 = (float)(1.0 - beta2);
+    a.bc2_sqrt = (float)std::sqrt(bc2);
+    a.eps = (float)eps;
+    const int grid = std::min(2048, grid_for(total, 256));
+    hipLaunchKernelGGL(adamw_kernel, dim3(grid), dim3(256), 0, S(stream), a);
+    if (launch_check("adamw_kernel")) return -1;
+  }
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,470 @@
+// Fused CodeNeRF MLP chain kernels for gfx950 (forward and dX-backward).
+//
+// Replaces CodeNeRF.forward (reference src/model.py:36-53) and the dX part of
+// its autograd backward (src/trainer.py:82) for a whole batch of samples in
+// ONE launch each:
+//
+//   * a wave owns 32 samples for the whole chain; every activation lives in
+//     registers (accumulator = next layer's B operand, see cn_layout.h);
+//   * positional encoding (src/model.py:4-7) is computed in registers from the
+//     sample position (or from ray origin/direction/z: src/utils.py:30);
+//   * weights stream through a 4-slot LDS ring of 16 KiB chunks filled by
+//     LDS-DMA (global_load_lds_dwordx4) 3 chunks ahead of use and shared by
+//     all waves of the workgroup; one raw s_barrier per chunk and a counted
+//     `s_waitcnt vmcnt(N)` whose N is computed at compile time from the static
+//     schedule (including the epilogue stores issued in between);
+//   * biases are the accumulators' initial value; the latent-code injection
+//     y + z_j (src/model.py:41-43,49-51) is folded into a per-object bias
+//     b_j + W_j z_j computed once per call (latent.hip);
+//   * ReLU, the sigma head (Softplus, threshold 20) and the rgb head are fused
+//     into the layer epilogues; for training the epilogues also write the
+//     layer outputs (for dW) and one sign bit per pre-activation (ReLU mask
+//     for the dX chain) with a single v_alignbit per value.
+#include "cn_common.h"
+#include "cn_sched.h"
+#include "chain_args.h"
+
+namespace cn {
+
+template <int P> struct PT;
+template <> struct PT<CN_P_BF16> {
+  using E = __bf16;
+  using BinT = u32x4;            // 8 bf16 packed in 4 dwords (one MFMA B operand)
+  static constexpr int kBin = 18;
+};
+template <> struct PT<CN_P_FP32> {
+  using E = float;
+  using BinT = float;            // one v_mfma_f32_32x32x2_f32 B operand
+  static constexpr int kBin = 144;
+};
+
+CN_DEV uint32_t pack_bf16x2(float lo, float hi) {
+  typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+  bf16x2 p = bf16x2{(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(uint32_t, p);
+}
+// ReLU of two packed bf16: signed-int16 max with 0 (negative and -0 -> +0)
+CN_DEV uint32_t relu_bf16x2(uint32_t x) {
+  typedef __attribute__((ext_vector_type(2))) short s16x2;
+  s16x2 v = __builtin_bit_cast(s16x2, x);
+  v = __builtin_elementwise_max(v, s16x2{0, 0});
+  return __builtin_bit_cast(uint32_t, v);
+}
+// shift the sign bit of v into the running mask word (one v_alignbit_b32)
+CN_DEV uint32_t push_sign(uint32_t bits, float v) {
+  return __builtin_amdgcn_alignbit(bits, __builtin_bit_cast(uint32_t, v), 31);
+}
+
+template <int P, int SB, int TB, bool BWD, int WAVES, bool TRAIN>
+struct Chain {
+  using S = Sched<P, SB, TB, BWD>;
+  using N = Net<SB, TB>;
+  using E = typename PT<P>::E;
+  using BinT = typename PT<P>::BinT;
+  static constexpr int kBin = PT<P>::kBin;
+  static constexpr bool kBf16 = (P == CN_P_BF16);
+  static constexpr int NL = S::NL;
+  static constexpr int kChunks = S::kChunks;
+  static constexpr int G = kChunkBlocks / WAVES;   // LDS-DMA instructions per wave per chunk
+  static constexpr int D = 3;                      // chunks in flight ahead of compute
+  static constexpr int NS = D + 1;                 // ring slots
+  static constexpr int kRingBytes = NS * kChunkBytes;
+  static constexpr int kBlobFloats = BiasBlob<SB, TB>::kFloats;
+  static constexpr int kWsOff = BiasBlob<SB, TB>::kWs;
+  static constexpr int kMiscOff = BiasBlob<SB, TB>::kMisc;
+  static constexpr int kDirStash = kBf16 ? 32 : 64;      // bytes per lane
+  static constexpr int kDirOff = kRingBytes + kBlobFloats * 4;
+  static constexpr int kMaskOff = kDirOff + (BWD ? 0 : WAVES * 64 * kDirStash);
+  static constexpr int kLdsBytes = kMaskOff + (BWD ? WAVES * N::kMasks * 1024 : 0);
+  static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
+  static_assert(kChunkBlocks % WAVES == 0, "waves must divide a chunk");
+  static_assert(N::kPlanes <= kMaxPlanes, "too many planes");
+  static_assert(kBlobFloats % 4 == 0, "blob alignment");
+
+  // ---------------- compile-time vmcnt bookkeeping
+  // Number of vector-memory instructions each wave issues in a layer epilogue.
+  static constexpr int stores_of_layer(int i) {
+    const Layer l = S::L(i);
+    if (!BWD) {
+      int s = 0;
+      if (TRAIN && l.plane >= 0) s += l.T * 4;
+      if (TRAIN && l.mask >= 0) s += 1;
+      if (l.epi == EPI_SHAPE) s += TRAIN ? 2 : 1;
+      return s;   // EPI_RGB stores come after the last wait: not counted (safe)
+    }
+    return l.T * 4;
+  }
+  static constexpr int stores_in_chunk(int c) {
+    int s = 0;
+    for (int i = 0; i < NL; ++i)
+      if (S::last_block(i) / kChunkBlocks == c) s += stores_of_layer(i);
+    return s;
+  }
+  static constexpr int issued(int i) { return i < kChunks ? G : 0; }
+  // Younger VMEM ops that may still be in flight when chunk c must have landed.
+  static constexpr int vm_wait(int c) {
+    int n = 0;
+    if (c < D) {
+      for (int i = c + 1; i < D; ++i) n += issued(i);
+      for (int i = 0; i < c; ++i) n += issued(i + D) + stores_in_chunk(i);
+    } else {
+      n += stores_in_chunk(c - D);
+      for (int i = c - D + 1; i < c; ++i) n += issued(i + D) + stores_in_chunk(i);
+    }
+    return n;
+  }
+
+  // ---------------- kernel body
+  __device__ static void run(const ChainArgs& a) {
+    __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int h = lane >> 5;
+    const int m = blockIdx.x * (WAVES * 32) + w * 32 + (lane & 31);
+    const int mc = m < a.M ? m : a.M - 1;
+    const int wglob = blockIdx.x * WAVES + w;
+    float* prm = (float*)(smem + kRingBytes);
+
+    // -- per-call bias blob -> LDS (plain loads; nothing is in flight yet)
+    for (int i = threadIdx.x; i < kBlobFloats / 4; i += WAVES * 64)
+      ((f32x4*)prm)[i] = ((const f32x4*)a.bias)[i];
+
+    BinT bin[kBin];
+    f32x16 acc[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc[t] = f32x16{};
+#pragma unroll
+    for (int q = 0; q < kBin; ++q) bin[q] = BinT{};
+
+    float ds = 0.f;   // bwd: sigma-head pre-activation gradient of this sample
+    if constexpr (!BWD) {
+      prologue_fwd(a, bin, smem, h, lane, w, m, mc);
+    } else {
+      ds = prologue_bwd(a, bin, smem, h, lane, w, m, mc, wglob);
+    }
+    __syncthreads();
+    if constexpr (!BWD) load_bias<0>(acc, prm, h);
+
+    static_for<0, D>([&](auto i) { issue<i>(a, smem, w, lane); });
+
+    float sig_part = 0.f;
+    static_for<0, kChunks>([&](auto cc) {
+      constexpr int c = cc;
+      wait_vmcnt<vm_wait(c)>();
+      block_barrier();
+      if constexpr (c + D < kChunks) issue<c + D>(a, smem, w, lane);
+      const char* slot = smem + (c % NS) * kChunkBytes + lane * 16;
+      static_for<0, kChunkBlocks>([&](auto bb) {
+        constexpr int g = c * kChunkBlocks + bb;
+        if constexpr (g < S::kBlocks) {
+          constexpr int li = S::layer_of(g);
+          constexpr int lb = g - S::first_block(li);
+          constexpr int t = lb / S::bpt(li);
+          constexpr int kb = lb % S::bpt(li);
+          const char* ap = slot + bb * kBlockBytes;
+          if constexpr (kBf16) {
+            const bf16x8 A = *(const bf16x8*)ap;
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                A, __builtin_bit_cast(bf16x8, bin[kb]), acc[t], 0, 0, 0);
+          } else {
+            const f32x4 A = *(const f32x4*)ap;
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[0], bin[4 * kb + 0], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[1], bin[4 * kb + 1], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[2], bin[4 * kb + 2], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[3], bin[4 * kb + 3], acc[t], 0, 0, 0);
+          }
+          if constexpr (g == S::last_block(li)) {
+            if constexpr (!BWD)
+              epilogue_fwd<li>(a, bin, acc, prm, smem, h, lane, w, m, wglob, sig_part);
+            else
+              epilogue_bwd<li>(a, bin, acc, prm, smem, h, lane, w, m, ds);
+          }
+        }
+      });
+    });
+  }
+
+  template <int C>
+  __device__ static void issue(const ChainArgs& a, char* smem, int w, int lane) {
+    const char* src = (const char*)a.wpack + (size_t)C * kChunkBytes + w * G * kBlockBytes + lane * 16;
+    char* dst = smem + (C % NS) * kChunkBytes + w * G * kBlockBytes;
+#pragma unroll
+    for (int k = 0; k < G; ++k)
+      glds16(src + k * kBlockBytes, (lds_void*)(dst + k * kBlockBytes));
+  }
+
+  // accumulators <- bias of forward layer LI (rows 32t + 8g + 4h + i)
+  template <int LI>
+  __device__ static void load_bias(f32x16* acc, const float* prm, int h) {
+    constexpr int T = S::L(LI).T;
+    const float* b = prm + LI * 256 + 4 * h;
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 v = *(const f32x4*)(b + 32 * t + 8 * g);
+        acc[t][4 * g + 0] = v[0];
+        acc[t][4 * g + 1] = v[1];
+        acc[t][4 * g + 2] = v[2];
+        acc[t][4 * g + 3] = v[3];
+      }
+  }
+
+  // ---------------- prologues
+  __device__ static void prologue_fwd(const ChainArgs& a, BinT* bin, char* smem, int h, int lane,
+                                      int w, int m, int mc) {
+    float x[3], d[3];
+    if (a.mode == 0) {
+      for (int k = 0; k < 3; ++k) { x[k] = a.xyz[3 * mc + k]; d[k] = a.vdir[3 * mc + k]; }
+    } else {
+      const int r = mc / a.nsamp;
+      const int s = mc - r * a.nsamp;
+      const float z = a.zvals[r * a.z_stride + s];
+      for (int k = 0; k < 3; ++k) {
+        d[k] = a.rays_d[3 * r + k];
+        // xyz = ro + vd * z  (src/utils.py:30), no fused multiply-add
+        x[k] = fadd_rn(a.rays_o[3 * r + k], fmul_rn(d[k], z));
+      }
+    }
+    // positional encodings: this lane half's 32 PE slots and 16 dir slots
+    float pe[32], dp[16];
+    pe[0] = h ? x[2] : x[0];
+    pe[1] = h ? 0.f : x[1];
+#pragma unroll
+    for (int k = 0; k < 15; ++k) {
+      const int p = 15 * h + k;
+      const int comp = p % 3, oct = p / 3;
+      const float v = (comp == 0 ? x[0] : comp == 1 ? x[1] : x[2]) * (float)(1 << oct);
+      float sn, cs;
+      sincosf(v, &sn, &cs);
+      pe[2 + 2 * k] = sn;
+      pe[3 + 2 * k] = cs;
+    }
+    dp[0] = h ? d[2] : d[0];
+    dp[1] = h ? 0.f : d[1];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      const int p = h ? (k < 5 ? 7 + k : -1) : k;
+      float sn = 0.f, cs = 0.f;
+      if (p >= 0) {
+        const int comp = p % 3, oct = p / 3;
+        const float v = (comp == 0 ? d[0] : comp == 1 ? d[1] : d[2]) * (float)(1 << oct);
+        sincosf(v, &sn, &cs);
+      }
+      dp[2 + 2 * k] = sn;
+      dp[3 + 2 * k] = cs;
+    }
+    // dir operand is needed only by the viewdir layer: stash it in LDS
+    char* stash = smem + kDirOff + (w * 64 + lane) * kDirStash;
+    if constexpr (kBf16) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        bin[q] = u32x4{pack_bf16x2(pe[8 * q + 0], pe[8 * q + 1]), pack_bf16x2(pe[8 * q + 2], pe[8 * q + 3]),
+                       pack_bf16x2(pe[8 * q + 4], pe[8 * q + 5]), pack_bf16x2(pe[8 * q + 6], pe[8 * q + 7])};
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        ((u32x4*)stash)[q] = u32x4{pack_bf16x2(dp[8 * q + 0], dp[8 * q + 1]), pack_bf16x2(dp[8 * q + 2], dp[8 * q + 3]),
+                                   pack_bf16x2(dp[8 * q + 4], dp[8 * q + 5]), pack_bf16x2(dp[8 * q + 6], dp[8 * q + 7])};
+    } else {
+#pragma unroll
+      for (int q = 0; q < 32; ++q) bin[q] = pe[q];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        ((f32x4*)stash)[q] = f32x4{dp[4 * q], dp[4 * q + 1], dp[4 * q + 2], dp[4 * q + 3]};
+    }
+    if constexpr (TRAIN) {
+      const auto rp = mkrsrc(a.pe);
+      const uint32_t op = ((uint32_t)m * 64 + h * 32) * sizeof(E);
+#pragma unroll
+      for (int q = 0; q < 32; q += 4) bstore4<E>(rp, op, q * sizeof(E), pe[q], pe[q + 1], pe[q + 2], pe[q + 3]);
+      const auto rd = mkrsrc(a.dir);
+      const uint32_t od = ((uint32_t)m * 32 + h * 16) * sizeof(E);
+#pragma unroll
+      for (int q = 0; q < 16; q += 4) bstore4<E>(rd, od, q * sizeof(E), dp[q], dp[q + 1], dp[q + 2], dp[q + 3]);
+    }
+  }
+
+  __device__ static float prologue_bwd(const ChainArgs& a, BinT* bin, char* smem, int h, int lane,
+                                       int w, int m, int mc, int wglob) {
+    const float g0 = a.drgb[3 * mc + 0], g1 = a.drgb[3 * mc + 1], g2 = a.drgb[3 * mc + 2];
+    // Softplus backward exactly as torch: grad * (x > 20 ? 1 : e^x / (e^x + 1))
+    const float s = a.spre[mc];
+    const float ex = expf(s);
+    const float ds = a.dsigma[mc] * (s > 20.f ? 1.f : ex / (ex + 1.f));
+    if constexpr (kBf16) {
+      // k-step 0, lane half h, element j -> drgb component 8h + j
+      if (h == 0) bin[0] = u32x4{pack_bf16x2(g0, g1), pack_bf16x2(g2, 0.f), 0u, 0u};
+    } else {
+      // k-step q, lane half h -> drgb component 2q + h
+      bin[0] = h ? g1 : g0;
+      bin[1] = h ? 0.f : g2;
+    }
+    {
+      // drgb as a padded [M][32] plane for the rgb-head weight gradient
+      const auto r8 = mkrsrc(a.d8);
+      const uint32_t o8 = ((uint32_t)m * 32 + h * 16) * sizeof(E);
+      bstore4<E>(r8, o8, 0, h ? 0.f : g0, h ? 0.f : g1, h ? 0.f : g2, 0.f);
+#pragma unroll
+      for (int q = 4; q < 16; q += 4) bstore4<E>(r8, o8, q * sizeof(E), 0.f, 0.f, 0.f, 0.f);
+      // the sigma-head gradient rides in columns 256 (value) and 257 (its
+      // rounding residual, so bf16 storage keeps ~16 significant bits) of the
+      // viewdir dA plane
+      const auto rv = mkrsrc(a.dA[SB + 2]);
+      const uint32_t ov = ((uint32_t)m * 288 + 256 + h * 16) * sizeof(E);
+      const float ds_hi = (float)(E)ds;
+      bstore4<E>(rv, ov, 0, h ? 0.f : ds_hi, h ? 0.f : ds - ds_hi, 0.f, 0.f);
+#pragma unroll
+      for (int q = 4; q < 16; q += 4) bstore4<E>(rv, ov, q * sizeof(E), 0.f, 0.f, 0.f, 0.f);
+    }
+    // ReLU sign bits of this wave -> LDS
+    const u32x4* src = (const u32x4*)a.masks + (size_t)wglob * N::kMasks * 64 + lane;
+    u32x4* dst = (u32x4*)(smem + kMaskOff) + (size_t)w * N::kMasks * 64 + lane;
+#pragma unroll
+    for (int k = 0; k < N::kMasks; ++k) dst[k * 64] = src[k * 64];
+    return ds;
+  }
+
+  // ---------------- epilogues
+  template <int LI>
+  __device__ static void epilogue_fwd(const ChainArgs& a, BinT* bin, f32x16* acc, const float* prm,
+                                      const char* smem, int h, int lane, int w, int m, int wglob,
+                                      float& sig_part) {
+    constexpr Layer l = S::L(LI);
+    if constexpr (l.epi == EPI_RGB) {
+      if (h == 0) {
+        a.rgb[3 * m + 0] = acc[0][0];
+        a.rgb[3 * m + 1] = acc[0][1];
+        a.rgb[3 * m + 2] = acc[0][2];
+      }
+      return;
+    } else {
+      uint32_t mbits[4] = {0u, 0u, 0u, 0u};
+      constexpr int yp = l.plane >= 0 ? l.plane : 0;
+      const auto ry = mkrsrc(a.Y[yp]);
+      const uint32_t oy = ((uint32_t)m * N::plane_width(yp) + 4 * h) * sizeof(E);
+      const float* ws = prm + kWsOff + 4 * h;
+#pragma unroll
+      for (int t = 0; t < l.T; ++t) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int row0 = 32 * t + 8 * g + 4 * h;
+          float v0 = acc[t][4 * g + 0], v1 = acc[t][4 * g + 1];
+          float v2 = acc[t][4 * g + 2], v3 = acc[t][4 * g + 3];
+          if constexpr (TRAIN && l.mask >= 0) {
+            uint32_t mb = mbits[t >> 1];
+            mb = push_sign(mb, v0); mb = push_sign(mb, v1);
+            mb = push_sign(mb, v2); mb = push_sign(mb, v3);
+            mbits[t >> 1] = mb;
+          }
+          if constexpr (l.epi == EPI_SHAPE) {
+            const f32x4 w4 = *(const f32x4*)(ws + 32 * t + 8 * g);
+            sig_part = __builtin_fmaf(w4[0], v0, sig_part);
+            sig_part = __builtin_fmaf(w4[1], v1, sig_part);
+            sig_part = __builtin_fmaf(w4[2], v2, sig_part);
+            sig_part = __builtin_fmaf(w4[3], v3, sig_part);
+          }
+          if constexpr (kBf16) {
+            uint32_t p0 = pack_bf16x2(v0, v1), p1 = pack_bf16x2(v2, v3);
+            if constexpr (l.epi == EPI_RELU) { p0 = relu_bf16x2(p0); p1 = relu_bf16x2(p1); }
+            BinT& b = bin[2 * t + (g >> 1)];
+            if ((g & 1) == 0) { b[0] = p0; b[1] = p1; } else { b[2] = p0; b[3] = p1; }
+            if constexpr (TRAIN && l.plane >= 0)
+              bstore64(ry, oy, u32x2{p0, p1}, (32 * t + 8 * g) * 2);
+          } else {
+            if constexpr (l.epi == EPI_RELU) {
+              v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+            }
+            bin[16 * t + 4 * g + 0] = v0;
+            bin[16 * t + 4 * g + 1] = v1;
+            bin[16 * t + 4 * g + 2] = v2;
+            bin[16 * t + 4 * g + 3] = v3;
+            if constexpr (TRAIN && l.plane >= 0)
+              bstore128(ry, oy, u32x4{f2u(v0), f2u(v1), f2u(v2), f2u(v3)}, (32 * t + 8 * g) * 4);
+          }
+        }
+      }
+      if constexpr (TRAIN && l.mask >= 0) {
+        bstore128(mkrsrc(a.masks), (((uint32_t)wglob * N::kMasks + l.mask) * 64 + lane) * 16,
+                  u32x4{mbits[0], mbits[1], mbits[2], mbits[3]});
+      }
+      if constexpr (l.epi == EPI_SHAPE) {
+        const float tot = sig_part + __shfl_xor(sig_part, 32);
+        const float pre = tot + prm[kMiscOff];
+        // both lane halves hold the full sum: every lane stores (same value,
+        // same address), so the store count per wave is fixed for vmcnt
+        bstore32(mkrsrc(a.sigma), (uint32_t)m * 4, f2u(softplus20(pre)));
+        if constexpr (TRAIN) bstore32(mkrsrc(a.spre), (uint32_t)m * 4, f2u(pre));
+      }
+      // the next layer (viewdir) takes the dir operand from the LDS stash
+      if constexpr (S::L(LI + 1).in_kind == IN_ACC_DIR) {
+        const char* stash = smem + kDirOff + (w * 64 + lane) * kDirStash;
+        if constexpr (kBf16) {
+          bin[16] = ((const u32x4*)stash)[0];
+          bin[17] = ((const u32x4*)stash)[1];
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const f32x4 v = ((const f32x4*)stash)[q];
+            bin[128 + 4 * q + 0] = v[0]; bin[128 + 4 * q + 1] = v[1];
+            bin[128 + 4 * q + 2] = v[2]; bin[128 + 4 * q + 3] = v[3];
+          }
+        }
+      }
+      load_bias<LI + 1>(acc, prm, h);
+    }
+  }
+
+  template <int LI>
+  __device__ static void epilogue_bwd(const ChainArgs& a, BinT* bin, f32x16* acc, const float* prm,
+                                      const char* smem, int h, int lane, int w, int m, float ds) {
+    constexpr Layer l = S::L(LI);
+    constexpr int width = N::dplane_width(l.plane);
+    const auto rdA = mkrsrc(a.dA[l.plane]);
+    const uint32_t odA = ((uint32_t)m * width + 4 * h) * sizeof(E);
+    u32x4 mw = u32x4{0u, 0u, 0u, 0u};
+    if constexpr (l.epi == EPI_BMASK)
+      mw = *(const u32x4*)(smem + kMaskOff + (((size_t)w * N::kMasks + l.mask) * 64 + lane) * 16);
+    const float* ws = prm + kWsOff + 4 * h;
+#pragma unroll
+    for (int t = 0; t < l.T; ++t) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int row0 = 32 * t + 8 * g + 4 * h;
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v[i] = acc[t][4 * g + i];
+          if constexpr (l.epi == EPI_BMASK) {
+            // sign bit of the forward pre-activation: set -> ReLU was off
+            const int pos = 31 - ((t & 1) * 16 + 4 * g + i);
+            const uint32_t off = (uint32_t)__builtin_amdgcn_sbfe((int)mw[t >> 1], pos, 1);
+            v[i] = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, v[i]) & ~off);
+          }
+        }
+        if constexpr (l.epi == EPI_BSIGMA) {
+          const f32x4 w4 = *(const f32x4*)(ws + 32 * t + 8 * g);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = fadd_rn(v[i], fmul_rn(ds, w4[i]));
+        }
+        if constexpr (kBf16) {
+          const uint32_t p0 = pack_bf16x2(v[0], v[1]), p1 = pack_bf16x2(v[2], v[3]);
+          BinT& b = bin[2 * t + (g >> 1)];
+          if ((g & 1) == 0) { b[0] = p0; b[1] = p1; } else { b[2] = p0; b[3] = p1; }
+          bstore64(rdA, odA, u32x2{p0, p1}, (32 * t + 8 * g) * 2);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) bin[16 * t + 4 * g + i] = v[i];
+          bstore128(rdA, odA, u32x4{f2u(v[0]), f2u(v[1]), f2u(v[2]), f2u(v[3])}, (32 * t + 8 * g) * 4);
+        }
+      }
+      acc[t] = f32x16{};
+    }
+  }
+};
+
+template <int P, int SB, int TB, bool BWD, int WAVES, bool TRAIN>
+__global__ __launch_bounds__(WAVES * 64, WAVES / 4) void chain_kernel(ChainArgs a) {
+  Chain<P, SB, TB, BWD, WAVES, TRAIN>::run(a);
+}
+
+}  // namespace cn

@@ -1,0 +1,50 @@
+// Argument block and per-call bias blob layout of the chain kernels.
+#pragma once
+#include <stdint.h>
+#include "cn_layout.h"
+
+namespace cn {
+
+constexpr int kMaxPlanes = 12;
+
+// Per-call bias blob (written by the latent kernel, read by the forward chain):
+//   [kFwdLayers][256]  bias of every forward layer (code injection folded in)
+//   [256]              sigma head weight (ws)
+//   [4]                misc: [0] sigma head bias
+template <int SB, int TB>
+struct BiasBlob {
+  static constexpr int kWs = Net<SB, TB>::kFwdLayers * 256;
+  static constexpr int kMisc = kWs + 256;
+  static constexpr int kFloats = kMisc + 4;
+};
+
+struct ChainArgs {
+  const void* wpack;       // packed weight blocks of this chain
+  const float* bias;       // per-call bias blob (BiasBlob layout)
+  int M;
+  // ---- forward inputs
+  int mode;                // 0: explicit points, 1: rays x samples
+  int nsamp;               // samples per ray (mode 1)
+  int z_stride;            // 0: shared z (reference), nsamp: per-ray z
+  const float* xyz;        // [M][3]            (mode 0)
+  const float* vdir;       // [M][3]            (mode 0)
+  const float* rays_o;     // [R][3]            (mode 1)
+  const float* rays_d;     // [R][3]            (mode 1)
+  const float* zvals;      // [z_stride ? R*nsamp : nsamp]
+  // ---- forward outputs (sized to the padded sample count)
+  float* sigma;            // [Mp]
+  float* rgb;              // [Mp][3]
+  // ---- activation workspace (training)
+  void* pe;                // [Mp][64]
+  void* dir;               // [Mp][32]
+  void* Y[kMaxPlanes];     // forward layer outputs
+  void* dA[kMaxPlanes];    // pre-activation gradients
+  void* d8;                // [Mp][32] drgb (padded)
+  float* spre;             // [Mp] sigma-head pre-activation
+  uint32_t* masks;         // [Mp/32][kMasks][64][4] pre-activation sign bits
+  // ---- backward inputs
+  const float* dsigma;     // [M]
+  const float* drgb;       // [M][3]
+};
+
+}  // namespace cn

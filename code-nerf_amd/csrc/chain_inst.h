@@ -1,0 +1,47 @@
+// Per-configuration kernel sets (one translation unit per precision x net).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+#include <vector>
+#include "chain_args.h"
+
+namespace cn {
+
+struct DwArgs;
+struct DwRedArgs;
+struct LatentArgs;
+struct LatentBwdArgs;
+
+struct ActLayout {
+  size_t pe = 0, dir = 0, Y[kMaxPlanes] = {}, dA[kMaxPlanes] = {}, d8 = 0, spre = 0, masks = 0, bytes = 0;
+};
+
+struct ChainSet {
+  int prec = 0, SB = 0, TB = 0;
+  int waves = 0;                 // waves per workgroup of the chain kernels
+  int tile = 0;                  // samples per chain workgroup
+  int n_params = 0, n_inject = 0, n_fwd_layers = 0;
+  size_t pack_fwd_bytes = 0, pack_bwd_bytes = 0;
+  int blob_floats = 0;
+  void (*fwd_train)(ChainArgs) = nullptr;
+  void (*fwd_infer)(ChainArgs) = nullptr;
+  void (*bwd)(ChainArgs) = nullptr;
+  void (*latent_fwd)(LatentArgs) = nullptr;
+  void (*latent_bwd)(LatentBwdArgs) = nullptr;
+  void (*code_grad)(LatentBwdArgs) = nullptr;
+  std::vector<int32_t> (*fwd_table)() = nullptr;
+  std::vector<int32_t> (*bwd_table)() = nullptr;
+  ActLayout (*layout)(size_t Mp) = nullptr;
+  // fills the dW / reduce argument blocks; returns the number of dW workgroups
+  int (*dw_setup)(char* act, int M, const float* zvec, float* dbuf, char* ws, DwArgs* dw,
+                  DwRedArgs* red) = nullptr;
+  size_t (*dw_ws_bytes)(int M) = nullptr;
+};
+
+ChainSet chain_set_fp32_3_1();
+ChainSet chain_set_bf16_3_1();
+ChainSet chain_set_fp32_2_1();
+ChainSet chain_set_bf16_2_1();
+
+}  // namespace cn

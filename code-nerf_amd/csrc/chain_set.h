@@ -1,0 +1,219 @@
+// Host-side construction of a ChainSet: packing tables (weight element ->
+// reference tensor element), activation-workspace layout, dW problem setup.
+// Included by the per-configuration translation units.
+#pragma once
+#include <algorithm>
+#include "chain.hip"
+#include "chain_inst.h"
+#include "dw_args.h"
+#include "latent.hip"
+
+namespace cn {
+
+template <int SB>
+constexpr int real_in_width(int L, int TB) {
+  // reference input width of forward layer L (src/model.py:19-34)
+  return L == 0 ? 63 : (L == SB + 2 ? 256 + 27 : (L == SB + TB + 4 ? 128 : 256));
+}
+
+inline int32_t src_idx(int tensor, int offset) { return (int32_t)(((uint32_t)tensor << 24) | (uint32_t)offset); }
+
+template <int P, int SB, int TB, bool BWD>
+std::vector<int32_t> build_pack_table() {
+  using S = Sched<P, SB, TB, BWD>;
+  using N = Net<SB, TB>;
+  constexpr bool bf16 = P == CN_P_BF16;
+  constexpr int EPL = S::elems_per_lane();
+  std::vector<int32_t> tab((size_t)S::kChunks * kChunkBlocks * 64 * EPL, -1);
+  for (int g = 0; g < S::kBlocks; ++g) {
+    const int li = S::layer_of(g);
+    const Layer l = S::L(li);
+    const int lb = g - S::first_block(li);
+    const int t = lb / S::bpt(li), kb = lb % S::bpt(li);
+    for (int lane = 0; lane < 64; ++lane) {
+      const int n = lane & 31, h = lane >> 5;
+      const int row = 32 * t + n;
+      for (int e = 0; e < EPL; ++e) {
+        int32_t v = -1;
+        if (!BWD) {
+          const int in_real = real_in_width<SB>(li, TB);
+          const int out_real = li == N::kFwdLayers - 1 ? 3 : l.T * 32;
+          int f = -1;
+          if (bf16) {
+            const int q = kb, j = e;
+            if (l.in_kind == IN_PE) f = pe_slot_feature(h, 8 * q + j);
+            else if (l.in_kind == IN_ACC_DIR && q >= 16) {
+              const int d = dir_slot_feature(h, 8 * (q - 16) + j);
+              f = d < 0 ? -1 : 256 + d;
+            } else f = bf16_acc_feature(q, h, j);
+          } else {
+            const int q = 4 * kb + e;
+            if (l.in_kind == IN_PE) f = pe_slot_feature(h, q);
+            else if (l.in_kind == IN_ACC_DIR && q >= 128) {
+              const int d = dir_slot_feature(h, q - 128);
+              f = d < 0 ? -1 : 256 + d;
+            } else f = f32_acc_feature(q, h);
+          }
+          if (f >= 0 && f < in_real && row < out_real) v = src_idx(l.w, row * in_real + f);
+        } else {
+          // transposed: output row = forward input feature, k = forward output feature
+          const int fl = li == 0 ? N::kFwdLayers - 1 : N::kFwdLayers - 1 - li;
+          const int in_f = real_in_width<SB>(fl, TB);
+          const int out_f = fl == N::kFwdLayers - 1 ? 3 : N::fwd(fl).T * 32;
+          int kf;
+          if (li == 0) kf = bf16 ? 8 * h + e : 2 * (4 * kb + e) + h;   // drgb component
+          else kf = bf16 ? bf16_acc_feature(kb, h, e) : f32_acc_feature(4 * kb + e, h);
+          if (kf < out_f && row < in_f) v = src_idx(l.w, kf * in_f + row);
+        }
+        tab[((size_t)g * 64 + lane) * EPL + e] = v;
+      }
+    }
+  }
+  return tab;
+}
+
+template <int P, int SB, int TB>
+ActLayout act_layout(size_t Mp) {
+  using N = Net<SB, TB>;
+  const size_t es = P == CN_P_BF16 ? 2 : 4;
+  ActLayout L;
+  size_t off = 0;
+  auto take = [&](size_t n) { size_t o = off; off += (n + 255) & ~(size_t)255; return o; };
+  L.pe = take(Mp * 64 * es);
+  L.dir = take(Mp * 32 * es);
+  for (int p = 0; p < N::kPlanes; ++p) L.Y[p] = take(Mp * N::plane_width(p) * es);
+  for (int p = 0; p < N::kPlanes; ++p) L.dA[p] = take(Mp * N::dplane_width(p) * es);
+  L.d8 = take(Mp * 32 * es);
+  L.spre = take(Mp * 4);
+  L.masks = take(Mp / 32 * N::kMasks * 64 * 16);
+  L.bytes = off;
+  return L;
+}
+
+// dW job geometry for M samples: slices and per-problem tile counts
+template <int SB, int TB>
+struct DwGeom {
+  using N = Net<SB, TB>;
+  static constexpr int NP = N::kFwdLayers;
+  int out_valid[NP], in_valid[NP], out_tiles[NP], in_tiles[NP];
+  int tiles = 0, slices = 1, mchunk = 32;
+  DwGeom(int M) {
+    for (int L = 0; L < NP; ++L) {
+      const bool last = L == NP - 1;
+      out_valid[L] = last ? 3 : (L == SB + 2 ? 258 : N::dplane_width(L));
+      in_valid[L] = L == 0 ? 64 : (L == SB + 2 ? 288 : (last ? 128 : 256));
+      out_tiles[L] = (out_valid[L] + 127) / 128;
+      in_tiles[L] = (in_valid[L] + 127) / 128;
+      tiles += out_tiles[L] * in_tiles[L];
+    }
+    const int steps = std::max(1, (M + 31) / 32);
+    slices = std::max(1, std::min(std::min(16, steps), (512 + tiles - 1) / tiles));
+    mchunk = ((steps + slices - 1) / slices) * 32;
+    slices = std::max(1, (M + mchunk - 1) / mchunk);
+  }
+  size_t part_floats(int L) const { return (size_t)slices * out_tiles[L] * 128 * in_tiles[L] * 128; }
+  size_t db_floats(int L) const { return (size_t)slices * out_tiles[L] * 128; }
+  size_t ws_bytes() const {
+    size_t s = 0;
+    for (int L = 0; L < NP; ++L) s += (part_floats(L) + db_floats(L)) * 4 + 512;
+    return s;
+  }
+};
+
+template <int P, int SB, int TB>
+size_t dw_ws_bytes(int M) { return DwGeom<SB, TB>(M).ws_bytes(); }
+
+template <int P, int SB, int TB>
+int dw_setup(char* act, int M, const float* zvec, float* dbuf, char* ws, DwArgs* dw, DwRedArgs* red) {
+  using N = Net<SB, TB>;
+  constexpr ParamIdx PI{SB, TB};
+  const DwGeom<SB, TB> G(M);
+  const int Mp = ((M + 255) / 256) * 256;
+  const ActLayout A = act_layout<P, SB, TB>(Mp);
+  static_assert(N::kFwdLayers <= kDwMaxProblems, "dw problems");
+  *dw = DwArgs{};
+  *red = DwRedArgs{};
+  dw->nprob = red->nprob = N::kFwdLayers;
+  dw->M = M;
+  dw->slices = red->slices = G.slices;
+  dw->mchunk = G.mchunk;
+  size_t off = 0;
+  int tp = 0, ep = 0;
+  for (int L = 0; L < N::kFwdLayers; ++L) {
+    const bool last = L == N::kFwdLayers - 1;
+    DwProblem& p = dw->p[L];
+    p.A = act + (last ? A.d8 : A.dA[L]);
+    p.lda = last ? 32 : N::dplane_width(L);
+    p.a_valid = G.out_valid[L];
+    if (L == 0) { p.X0 = act + A.pe; p.ldx0 = 64; p.x0_cols = 64; }
+    else if (L == SB + 2) {
+      p.X0 = act + A.Y[SB + 1]; p.ldx0 = 256; p.x0_cols = 256;
+      p.X1 = act + A.dir; p.ldx1 = 32;
+    } else { p.X0 = act + A.Y[L - 1]; p.ldx0 = N::plane_width(L - 1); p.x0_cols = p.ldx0; }
+    if (!p.X1) { p.X1 = p.X0; p.ldx1 = p.ldx0; }
+    p.in_valid = G.in_valid[L];
+    p.out_tiles = G.out_tiles[L];
+    p.in_tiles = G.in_tiles[L];
+    p.part = (float*)(ws + off);
+    off += ((G.part_floats(L) * 4 + 255) & ~(size_t)255);
+    p.dbpart = (float*)(ws + off);
+    off += ((G.db_floats(L) * 4 + 255) & ~(size_t)255);
+    dw->tile_prefix[L] = tp;
+    tp += p.out_tiles * p.in_tiles;
+
+    DwRedProblem& r = red->p[L];
+    r.part = p.part;
+    r.dbpart = p.dbpart;
+    r.ldp = p.in_tiles * 128;
+    r.rows_pad = p.out_tiles * 128;
+    r.out_real = last ? 3 : N::fwd(L).T * 32;
+    r.in_real = real_in_width<SB>(L, TB);
+    r.cols = p.in_valid;
+    r.map = L == 0 ? MAP_PE : (L == SB + 2 ? MAP_VIEWDIR : MAP_PLAIN);
+    r.w = N::fwd(L).w;
+    r.b = N::fwd(L).b;
+    r.w2 = PI.sigma_w();
+    r.b2 = PI.sigma_w() + 1;
+    const int inj = L >= 1 ? N::fwd(L - 1).inj : -1;
+    r.z = inj >= 0 ? zvec + inj * 256 : nullptr;
+    r.dbout = inj >= 0 ? dbuf + inj * 256 : nullptr;
+    r.elems = (r.out_real + (L == SB + 2 ? 2 : 0)) * r.cols;
+    red->prefix[L] = ep;
+    ep += r.elems;
+  }
+  dw->tile_prefix[N::kFwdLayers] = tp;
+  red->prefix[N::kFwdLayers] = ep;
+  return tp * G.slices;
+}
+
+template <int P, int SB, int TB>
+ChainSet make_chain_set() {
+  using N = Net<SB, TB>;
+  constexpr int WAVES = P == CN_P_BF16 ? 8 : 4;
+  ChainSet s;
+  s.prec = P;
+  s.SB = SB;
+  s.TB = TB;
+  s.waves = WAVES;
+  s.tile = WAVES * 32;
+  s.n_params = ParamIdx{SB, TB}.count();
+  s.n_inject = N::kInject;
+  s.n_fwd_layers = N::kFwdLayers;
+  s.pack_fwd_bytes = Sched<P, SB, TB, false>::packed_bytes();
+  s.pack_bwd_bytes = Sched<P, SB, TB, true>::packed_bytes();
+  s.blob_floats = BiasBlob<SB, TB>::kFloats;
+  s.fwd_train = chain_kernel<P, SB, TB, false, WAVES, true>;
+  s.fwd_infer = chain_kernel<P, SB, TB, false, WAVES, false>;
+  s.bwd = chain_kernel<P, SB, TB, true, WAVES, true>;
+  s.latent_fwd = latent_fwd_kernel<SB, TB>;
+  s.latent_bwd = latent_bwd_kernel<SB, TB>;
+  s.code_grad = code_grad_kernel<SB, TB>;
+  s.fwd_table = build_pack_table<P, SB, TB, false>;
+  s.bwd_table = build_pack_table<P, SB, TB, true>;
+  s.layout = act_layout<P, SB, TB>;
+  s.dw_setup = dw_setup<P, SB, TB>;
+  s.dw_ws_bytes = dw_ws_bytes<P, SB, TB>;
+  return s;
+}
+
+}  // namespace cn

@@ -1,0 +1,108 @@
+// Shared device/host definitions for the CodeNeRF gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <type_traits>
+#include <utility>
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+
+#define CN_DEV __device__ __forceinline__
+
+// ---------------------------------------------------------------- precision
+enum { CN_P_FP32 = 0, CN_P_BF16 = 1 };
+
+// Compile-time for loop: f(std::integral_constant<int, I>) for I in [0, N).
+template <int Begin, int End, class F>
+CN_DEV void static_for(F&& f) {
+  if constexpr (Begin < End) {
+    f(std::integral_constant<int, Begin>{});
+    static_for<Begin + 1, End>(f);
+  }
+}
+
+// LDS pointer type for the LDS-DMA builtin.
+typedef __attribute__((address_space(3))) void lds_void;
+
+CN_DEV void glds16(const void* gsrc, lds_void* ldst) {
+  // LDS-DMA: the wave writes 64 x 16 B contiguously at ldst (wave-uniform);
+  // each lane supplies its own global source address.
+  __builtin_amdgcn_global_load_lds(gsrc, ldst, 16, 0, 0);
+}
+
+template <int N>
+CN_DEV void wait_vmcnt() {
+  static_assert(N >= 0, "vmcnt");
+  constexpr int n = N > 63 ? 63 : N;
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n) : "memory");
+}
+
+CN_DEV void block_barrier() {
+  // raw s_barrier: does not drain in-flight LDS-DMA (unlike __syncthreads).
+  // lgkmcnt(0) first: this wave's LDS reads of the slot about to be refilled
+  // must have returned before any wave issues the DMA into it.  The asm
+  // memory clobbers stop the compiler moving LDS accesses across.
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+CN_DEV float bf2f(__bf16 x) { return (float)x; }
+
+// Softplus(beta=1, threshold=20) as torch.nn.Softplus.
+CN_DEV float softplus20(float x) { return x > 20.f ? x : log1pf(expf(x)); }
+
+// Exact (non-contracted) fp32 helpers so host-reference rounding is
+// reproduced.  hipcc defaults to -ffp-contract=fast, which fuses a*b+c into an
+// FMA even through __fmul_rn/__fadd_rn once inlined; the pragma keeps these
+// operations un-fusable.
+CN_DEV float fmul_rn(float a, float b) {
+#pragma clang fp contract(off)
+  return a * b;
+}
+CN_DEV float fadd_rn(float a, float b) {
+#pragma clang fp contract(off)
+  return a + b;
+}
+
+// 4 consecutive elements of an activation plane (fp32 or bf16 storage)
+template <class E> CN_DEV void store4(E* p, float a, float b, float c, float d);
+template <> CN_DEV void store4<float>(float* p, float a, float b, float c, float d) {
+  *(f32x4*)p = f32x4{a, b, c, d};
+}
+template <> CN_DEV void store4<__bf16>(__bf16* p, float a, float b, float c, float d) {
+  *(bf16x4*)p = bf16x4{(__bf16)a, (__bf16)b, (__bf16)c, (__bf16)d};
+}
+
+// ---- buffer stores: descriptor in SGPRs, 32-bit per-lane offset, the
+// compile-time part of the address folded into the instruction offset.
+CN_DEV __amdgpu_buffer_rsrc_t mkrsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, -1, 0x00020000);
+}
+// `soff` is wave-uniform (an SGPR / inline constant), so compile-time
+// address parts never cost a VGPR.
+CN_DEV void bstore32(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t v, int soff = 0) {
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)off, soff, 0);
+}
+CN_DEV void bstore64(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x2 v, int soff = 0) {
+  __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)off, soff, 0);
+}
+CN_DEV void bstore128(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v, int soff = 0) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, soff, 0);
+}
+CN_DEV uint32_t f2u(float x) { return __builtin_bit_cast(uint32_t, x); }
+// 4 consecutive plane elements through a buffer descriptor
+template <class E> CN_DEV void bstore4(__amdgpu_buffer_rsrc_t r, uint32_t off, int soff, float a, float b, float c, float d);
+template <> CN_DEV void bstore4<float>(__amdgpu_buffer_rsrc_t r, uint32_t off, int soff, float a, float b, float c, float d) {
+  bstore128(r, off, u32x4{f2u(a), f2u(b), f2u(c), f2u(d)}, soff);
+}
+template <> CN_DEV void bstore4<__bf16>(__amdgpu_buffer_rsrc_t r, uint32_t off, int soff, float a, float b, float c, float d) {
+  bf16x4 v = bf16x4{(__bf16)a, (__bf16)b, (__bf16)c, (__bf16)d};
+  bstore64(r, off, __builtin_bit_cast(u32x2, v), soff);
+}

@@ -1,0 +1,161 @@
+// Static description of the CodeNeRF MLP as a chain of MFMA layers.
+//
+// Shared by the host plan builder (packing / gradient-mapping tables) and the
+// chain kernels (compile-time block schedule).  The network is the reference
+// CodeNeRF (src/model.py:10-53) with W = latent_dim = 256, num_xyz_freq = 10,
+// num_dir_freq = 4; shape_blocks (SB) and texture_blocks (TB) are template
+// parameters.
+//
+// Orientation (both precisions): a wave owns 32 samples; an MFMA computes
+// Y^T[32 out features][32 samples] = W[32][K] * X^T[K][32 samples].  The
+// accumulator (32x32 f32: sample on the lane, features in 16 registers)
+// therefore IS the next layer's B operand after bias/activation, with the k
+// order permuted; the packed weights absorb that permutation.
+#pragma once
+#include <stdint.h>
+
+namespace cn {
+
+constexpr int kW = 256;
+constexpr int kLatent = 256;
+constexpr int kXyzFreq = 10;
+constexpr int kDirFreq = 4;
+constexpr int kPeSlots = 64;   // 63 PE features + 1 pad, 32 per lane half
+constexpr int kDirSlots = 32;  // 27 dir-PE features + 5 pad, 16 per lane half
+constexpr int kBlockBytes = 1024;        // one A-fragment block (64 lanes x 16 B)
+constexpr int kChunkBlocks = 16;         // LDS ring slot = 16 blocks = 16 KiB
+constexpr int kChunkBytes = kBlockBytes * kChunkBlocks;
+
+// Reference parameter tensor indices (state_dict order, oracle/params.py).
+struct ParamIdx {
+  int SB, TB;
+  constexpr int enc_xyz_w() const { return 0; }
+  constexpr int shape_latent_w(int j) const { return 2 + 4 * j; }      // j: 0-based block
+  constexpr int shape_w(int j) const { return 4 + 4 * j; }
+  constexpr int enc_shape_w() const { return 2 + 4 * SB; }
+  constexpr int sigma_w() const { return 4 + 4 * SB; }
+  constexpr int viewdir_w() const { return 6 + 4 * SB; }
+  constexpr int tex_latent_w(int j) const { return 8 + 4 * SB + 4 * j; }
+  constexpr int tex_w(int j) const { return 10 + 4 * SB + 4 * j; }
+  constexpr int rgb0_w() const { return 8 + 4 * SB + 4 * TB; }
+  constexpr int rgb2_w() const { return 10 + 4 * SB + 4 * TB; }
+  constexpr int count() const { return 12 + 4 * (SB + TB); }
+};
+
+enum InKind : int { IN_PE = 0, IN_ACC = 1, IN_ACC_DIR = 2, IN_DRGB = 3 };
+enum EpiKind : int {
+  EPI_RELU = 0,      // fwd: + bias, ReLU, (store Y, mask), (+ injection)
+  EPI_SHAPE = 1,     // fwd: + bias, no activation, sigma head (encoding_shape)
+  EPI_RGB = 2,       // fwd: + bias, rgb output (last layer)
+  EPI_BMASK = 3,     // bwd: dA = dY * mask, store dA
+  EPI_BSIGMA = 4,    // bwd: dA = dY + w_sigma * ds (no activation), store dA
+};
+
+struct Layer {
+  int T;          // output tiles of 32 features
+  int K;          // input features incl. padding (multiple of 16 bf16 / 8 fp32)
+  int in_kind;
+  int epi;
+  int w;          // weight tensor index (reference order)
+  int b;          // bias tensor index, -1 none
+  int inj;        // fwd: injection vector added to the output (next input), -1 none
+  int mask;       // fwd: mask slot written; bwd: mask slot read; -1 none
+  int plane;      // fwd: Y plane written; bwd: dA plane written; -1 none
+  int t_in;       // input tiles from the previous accumulator (K_acc / 32)
+};
+
+template <int SB, int TB>
+struct Net {
+  static constexpr int kFwdLayers = SB + TB + 5;
+  static constexpr int kBwdLayers = SB + TB + 4;
+  static constexpr int kPlanes = SB + TB + 4;       // Y / dA planes (all but last layer)
+  static constexpr int kMasks = SB + TB + 3;        // ReLU layers
+  static constexpr int kInject = SB + TB;
+  static constexpr ParamIdx P{SB, TB};
+
+  // forward layer i (0-based)
+  static constexpr Layer fwd(int i) {
+    if (i == 0) return {8, kPeSlots, IN_PE, EPI_RELU, P.enc_xyz_w(), P.enc_xyz_w() + 1,
+                        SB >= 1 ? 0 : -1, 0, 0, 0};
+    if (i <= SB) return {8, 256, IN_ACC, EPI_RELU, P.shape_w(i - 1), P.shape_w(i - 1) + 1,
+                         i < SB ? i : -1, i, i, 8};
+    if (i == SB + 1) return {8, 256, IN_ACC, EPI_SHAPE, P.enc_shape_w(), P.enc_shape_w() + 1,
+                             -1, -1, i, 8};
+    if (i == SB + 2) return {8, 256 + kDirSlots, IN_ACC_DIR, EPI_RELU, P.viewdir_w(),
+                             P.viewdir_w() + 1, TB >= 1 ? SB : -1, SB + 1, i, 8};
+    if (i <= SB + 2 + TB) {
+      int j = i - (SB + 3);
+      return {8, 256, IN_ACC, EPI_RELU, P.tex_w(j), P.tex_w(j) + 1,
+              j + 1 < TB ? SB + j + 1 : -1, i - 1, i, 8};
+    }
+    if (i == SB + TB + 3) return {4, 256, IN_ACC, EPI_RELU, P.rgb0_w(), P.rgb0_w() + 1, -1,
+                                  SB + TB + 2, i, 8};
+    return {1, 128, IN_ACC, EPI_RGB, P.rgb2_w(), P.rgb2_w() + 1, -1, -1, -1, 4};
+  }
+
+  // mask slot of forward layer f (or -1): ReLU layers in order
+  static constexpr int mask_of(int f) { return fwd(f).mask; }
+
+  // backward (dX) layer i in processing order; K in bf16 units (fp32 uses kdrgb8)
+  static constexpr Layer bwd(int i) {
+    const int last = SB + TB + 4;          // fwd index of rgb2
+    if (i == 0) {   // rgb2^T: drgb -> d y_rgb0 ; dA(rgb0) = * mask(rgb0)
+      return {4, 16, IN_DRGB, EPI_BMASK, P.rgb2_w(), -1, -1, mask_of(last - 1), last - 1, 0};
+    }
+    // i >= 1: transpose of forward layer f = last - i, producing dA of layer f - 1
+    const int f = last - i;
+    const Layer L = fwd(f);
+    const int tin = fwd(f).T;              // input = dA of layer f (its T tiles)
+    if (f == SB + 2) {   // viewdir^T (y part only) -> d y_shape (+ sigma head)
+      return {8, tin * 32, IN_ACC, EPI_BSIGMA, L.w, -1, -1, -1, f - 1, tin};
+    }
+    return {8, tin * 32, IN_ACC, EPI_BMASK, L.w, -1, -1, mask_of(f - 1), f - 1, tin};
+  }
+
+  static constexpr int plane_width(int p) { return p == SB + TB + 3 ? 128 : 256; }
+  // dA plane widths: viewdir's carries the sigma-head gradient in column 256
+  static constexpr int dplane_width(int p) {
+    return p == SB + TB + 3 ? 128 : (p == SB + 2 ? 288 : 256);
+  }
+};
+
+// ---- k-slot maps -------------------------------------------------------------
+// PE slot (lane half h, index s in 0..31) -> reference PE feature (-1 = pad).
+// Reference order (src/model.py:4-7): [x0 x1 x2, sin(a_0..a_29), cos(a_0..a_29)],
+// a_p = 2^(p/3) * x_(p%3).  Each lane half computes sin AND cos of the same
+// argument, so slots are (raw, raw, sin a_k, cos a_k, ...).
+inline constexpr int pe_slot_feature(int h, int s) {
+  if (s == 0) return h == 0 ? 0 : 2;
+  if (s == 1) return h == 0 ? 1 : -1;
+  int k = (s - 2) >> 1;                 // 0..14
+  int p = 15 * h + k;                   // argument index 0..29
+  return (s & 1) == 0 ? 3 + p : 33 + p;
+}
+// dir slot (h, s in 0..15) -> dir-PE feature (0..26) or -1
+inline constexpr int dir_slot_feature(int h, int s) {
+  if (s == 0) return h == 0 ? 0 : 2;
+  if (s == 1) return h == 0 ? 1 : -1;
+  int k = (s - 2) >> 1;
+  int p = h == 0 ? k : 7 + k;           // half 0: args 0..6, half 1: 7..11
+  if (h == 1 && k >= 5) return -1;
+  return (s & 1) == 0 ? 3 + p : 15 + p;
+}
+// argument index for the sincos pair at slot pair k of half h (-1 none)
+inline constexpr int pe_pair_arg(int h, int k) { return 15 * h + k; }
+inline constexpr int dir_pair_arg(int h, int k) {
+  return h == 0 ? k : (k < 5 ? 7 + k : -1);
+}
+
+// bf16 32x32x16: k-step q, lane half h, element j -> input index within K.
+// For accumulator-fed inputs: feature 32u + 16s + 8(j>>2) + 4h + (j&3), q = 2u+s.
+inline constexpr int bf16_acc_feature(int q, int h, int j) {
+  return 32 * (q >> 1) + 16 * (q & 1) + 8 * (j >> 2) + 4 * h + (j & 3);
+}
+// fp32 32x32x2: k-step q (= 16u + r), lane half h -> feature 32u + (r&3) + 8(r>>2) + 4h
+inline constexpr int f32_acc_feature(int q, int h) {
+  return 32 * (q >> 4) + ((q & 15) & 3) + 8 * ((q & 15) >> 2) + 4 * h;
+}
+// accumulator register r of lane half h -> row within the 32-row tile
+inline constexpr int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+}  // namespace cn

@@ -1,0 +1,132 @@
+/*
+ * codenerf.h -- C ABI of the MI355X (gfx950) CodeNeRF render/train hot path.
+ *
+ * The reference (yuliangguo/code-nerf) has no FFI: its hot path is a set of
+ * Python calls made by both loops (src/trainer.py:65-84, src/optimizer.py:
+ * 75-94).  Each entry point below replaces one of them; the comment names the
+ * reference interface (file:line) it stands in for.
+ *
+ * Conventions
+ *   - All buffers are DEVICE pointers owned by the caller (plain float32 unless
+ *     stated), all sizes are element counts, every call is asynchronous on the
+ *     given HIP stream (hipStream_t passed as void*; NULL = default stream).
+ *   - Return 0 on success, a negative code on error; cn_last_error() gives a
+ *     thread-local message.  No C++ exception crosses the ABI; no call
+ *     allocates device memory (workspaces are caller-provided, sized by the
+ *     cn_*_bytes queries).
+ *   - Parameters are addressed through a device array of float* in the
+ *     reference state_dict order (encoding_xyz.0.weight, encoding_xyz.0.bias,
+ *     shape_latent_layer_1.0.weight, ... rgb.2.bias; src/model.py:20-34);
+ *     gradients likewise (accumulated, like autograd's .grad).
+ *   - Sample index m = ray * n_samples + s (reference layout (R, N, ...)).
+ *     Per-sample outputs must be sized for cn_pad_samples(plan, M) samples.
+ */
+#ifndef CODENERF_H
+#define CODENERF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CN_ABI_VERSION 1
+#define CN_FP32 0 /* exact-fp32 MFMA path (parity) */
+#define CN_BF16 1 /* bf16 operands, fp32 accumulate (throughput) */
+
+typedef struct cn_plan cn_plan;
+
+int cn_abi_version(void);
+const char *cn_last_error(void);
+
+/* ---- plan: static layout for one network configuration and precision.
+ * Replaces CodeNeRF.__init__ (src/model.py:11-34).  Supported:
+ * W = latent_dim = 256, num_xyz_freq = 10, num_dir_freq = 4,
+ * (shape_blocks, texture_blocks) in {(3,1), (2,1)}. */
+int cn_plan_create(int shape_blocks, int texture_blocks, int W, int num_xyz_freq,
+                   int num_dir_freq, int latent_dim, int precision, cn_plan **out);
+void cn_plan_destroy(cn_plan *plan);
+int cn_plan_num_params(const cn_plan *plan);        /* tensors in the state_dict */
+int cn_plan_num_inject(const cn_plan *plan);        /* shape + texture blocks */
+int cn_pad_samples(const cn_plan *plan, int M);     /* M rounded to the tile */
+size_t cn_packed_bytes(const cn_plan *plan, int bwd); /* packed weights */
+size_t cn_blob_floats(const cn_plan *plan);         /* per-call bias blob */
+size_t cn_act_bytes(const cn_plan *plan, int M);    /* training activations */
+size_t cn_dw_ws_bytes(const cn_plan *plan, int M);  /* weight-grad partials */
+
+/* ---- weights: pack the parameters into the chain kernels' fragment order
+ * (fwd: W, bwd: W^T).  Call after every optimiser step. */
+int cn_pack_weights(const cn_plan *plan, const float *const *d_params, void *d_pack_fwd,
+                    void *d_pack_bwd, void *stream);
+
+/* ---- per-object latent layers, src/model.py:41,49: z_j = ReLU(L_j c + c_j),
+ * folded into the next layer's bias (b + W z).  d_blob: cn_blob_floats floats,
+ * d_zvec: num_inject x 256. */
+int cn_latent_fwd(const cn_plan *plan, const float *const *d_params, const float *d_shape_code,
+                  const float *d_texture_code, float *d_blob, float *d_zvec, void *stream);
+
+/* ---- CodeNeRF.forward (src/model.py:36-53) for M samples.
+ * mode A (d_xyz != NULL): explicit points xyz/viewdir [M][3];
+ * mode B (d_xyz == NULL): samples of rays, xyz = rays_o + rays_d * z
+ *   (src/utils.py:30), z = d_z[ray * z_stride + s] (z_stride 0: one z vector
+ *   shared by all rays as in the reference, n_samples: per-ray z).
+ * d_sigma [Mp], d_rgb [Mp][3].  d_act != NULL stores what the backward
+ * needs (cn_act_bytes(plan, M) bytes). */
+int cn_mlp_fwd(const cn_plan *plan, const void *d_pack_fwd, const float *d_blob, int M,
+               const float *d_xyz, const float *d_viewdir, const float *d_rays_o,
+               const float *d_rays_d, const float *d_z, int z_stride, int n_samples,
+               float *d_sigma, float *d_rgb, void *d_act, void *stream);
+
+/* ---- autograd of CodeNeRF.forward (src/trainer.py:82): dX chain. */
+int cn_mlp_bwd(const cn_plan *plan, const void *d_pack_bwd, const float *d_blob, int M,
+               const float *d_dsigma, const float *d_drgb, void *d_act, void *stream);
+
+/* ---- weight / bias gradients, accumulated into d_grads; d_dbuf
+ * (num_inject x 256) receives this call's bias gradient of every layer fed by
+ * a latent code (input of cn_latent_bwd). */
+int cn_mlp_dw(const cn_plan *plan, void *d_act, int M, const float *d_zvec,
+              float *const *d_grads, float *d_dbuf, void *d_ws, void *stream);
+
+/* ---- latent layers + code gradients (+ the code regulariser of
+ * src/trainer.py:76-78 when reg_coef != 0; d_reg_out += reg value).
+ * d_scratch: num_inject x 256 floats.  d_dshape / d_dtex accumulate. */
+int cn_latent_bwd(const cn_plan *plan, const float *const *d_params, float *const *d_grads,
+                  const float *d_shape_code, const float *d_texture_code, const float *d_zvec,
+                  const float *d_dbuf, float *d_scratch, float *d_dshape, float *d_dtex,
+                  float reg_coef, float *d_reg_out, void *stream);
+
+/* ---- geometry / rendering --------------------------------------------- */
+/* get_rays, src/utils.py:10-19.  d_c2w: 4x4 row-major.  focal_is_f64: the
+ * reference receives focal as a float64 tensor from default_collate and forms
+ * the camera directions in float64 (type promotion) before casting. */
+int cn_get_rays(int H, int W, double focal, int focal_is_f64, const float *d_c2w,
+                float *d_rays_o, float *d_viewdirs, void *stream);
+/* sample_from_rays point expansion, src/utils.py:30-31 */
+int cn_sample_points(const float *d_rays_o, const float *d_viewdirs, const float *d_z, int z_stride,
+                     int R, int N, float *d_xyz, float *d_viewdir_rep, void *stream);
+/* volume_rendering, src/utils.py:34-47 (N <= 256).  d_weights may be NULL. */
+int cn_composite_fwd(const float *d_sigma, const float *d_rgb, const float *d_z, int z_stride,
+                     int R, int N, int white_bg, float *d_out_rgb, float *d_out_depth,
+                     float *d_weights, void *stream);
+/* autograd of volume_rendering; d_grad_depth may be NULL */
+int cn_composite_bwd(const float *d_sigma, const float *d_rgb, const float *d_z, int z_stride,
+                     int R, int N, int white_bg, const float *d_grad_rgb,
+                     const float *d_grad_depth, float *d_dsigma, float *d_drgb, void *stream);
+/* training: composite + chunk-mean MSE (src/trainer.py:69,75; chunk = batch
+ * size B) + its gradient w.r.t. sigma / rgb.  d_chunk_loss: ceil(R/chunk). */
+int cn_render_loss(const float *d_sigma, const float *d_rgb, const float *d_z, int z_stride,
+                   int R, int N, int white_bg, const float *d_gt, int chunk, float *d_out_rgb,
+                   float *d_ray_se, float *d_chunk_loss, float *d_dsigma, float *d_drgb,
+                   void *stream);
+
+/* ---- torch.optim.AdamW step (src/trainer.py:116-120) over nseg tensors
+ * (host arrays of device pointers), step = 1-based count of this update. */
+int cn_adamw_step(int nseg, float *const *p, const float *const *g, float *const *m,
+                  float *const *v, const int *n, const double *lr, double weight_decay,
+                  double beta1, double beta2, double eps, int step, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CODENERF_H */
