@@ -1,0 +1,238 @@
+"""Benchmark: CodeNeRF training throughput on MI355X (ray-samples / second).
+
+Workload (BASELINE.json configs[1]): srncar.json network (3 shape blocks,
+1 texture block, W = 256), one 128x128 image per object per step, 64 coarse
++ 64 fine samples per ray (128 MLP evaluations per ray), bf16 MFMA with fp32
+accumulation, synthetic SRN-cars-like data (random target image, camera on a
+radius-1.3 sphere, focal 131.25, near/far 0.8/1.8; no dataset is available
+offline).  One step = rays -> samples -> CodeNeRF forward -> compositing +
+chunk-mean MSE (+ code regulariser) -> full backward (dX chain, dW, latent
+layers, code rows) -> [RCCL all-reduce of the gradients when N > 1] -> AdamW
+over the model and both code tables.  ``value`` = ray-samples of all ranks /
+max-over-ranks wall time of the K timed steps.
+
+Run:  python bench.py [--gpus N --steps K --warmup W]
+      (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py)
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+BF16_PEAK_TFLOPS = 2500.0       # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+FP32_PEAK_TFLOPS = 157.3        # fp32 MFMA
+HBM_PEAK_GBS = 8000.0
+FLOP_PER_SAMPLE = {"fwd": 899_328, "bwd": 853_248, "dw": 899_328}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--H", type=int, default=128)
+    ap.add_argument("--n-coarse", type=int, default=64)
+    ap.add_argument("--n-fine", type=int, default=64)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--objects", type=int, default=64)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def make_pose(radius, az_deg, el_deg):
+    az, el = math.radians(az_deg), math.radians(el_deg)
+    eye = torch.tensor([radius * math.cos(el) * math.sin(az), radius * math.sin(el),
+                        radius * math.cos(el) * math.cos(az)], dtype=torch.float64)
+    fwd = -eye / eye.norm()
+    up = torch.tensor([0.0, 1.0, 0.0], dtype=torch.float64)
+    right = torch.linalg.cross(fwd, up)
+    right = right / right.norm()
+    tup = torch.linalg.cross(right, fwd)
+    c2w = torch.eye(4, dtype=torch.float64)
+    c2w[:3, 0], c2w[:3, 1], c2w[:3, 2], c2w[:3, 3] = right, tup, -fwd, eye
+    return c2w.float()
+
+
+class Timers:
+    """HIP events around the kernels of one phase, on the launching stream."""
+
+    def __init__(self):
+        self.ev = {}
+        self.on = False
+
+    def mark(self, name):
+        if not self.on:
+            return None
+        s = torch.cuda.Event(enable_timing=True)
+        s.record()
+        return s
+
+    def done(self, name, s):
+        if s is None:
+            return
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        self.ev.setdefault(name, []).append((s, e))
+
+    def summary(self):
+        return {k: sum(s.elapsed_time(e) for s, e in v) / len(v) for k, v in self.ev.items()}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from codenerf_amd.model import CodeNeRF
+    from codenerf_amd.trainer_core import TrainCore
+
+    torch.manual_seed(1234 + rank)
+    model = CodeNeRF(3, 1, precision=args.precision).to(dev)
+    if dist is not None:      # identical initial weights on every rank
+        for p in model.parameters():
+            dist.broadcast(p.data, 0)
+    n_obj = args.objects
+    shape_codes = torch.nn.Parameter(torch.randn(n_obj, 256, device=dev) / math.sqrt(128))
+    texture_codes = torch.nn.Parameter(torch.randn(n_obj, 256, device=dev) / math.sqrt(128))
+    if dist is not None:
+        dist.broadcast(shape_codes.data, 0)
+        dist.broadcast(texture_codes.data, 0)
+
+    H = W = args.H
+    focal = 131.25 * H / 128
+    R = H * W
+    timers = Timers()
+    core = TrainCore(model, shape_codes, texture_codes, near=0.8, far=1.8, n_coarse=args.n_coarse,
+                     n_fine=args.n_fine, chunk=2048, reg_coef=1e-4, lr=(1e-4, 1e-3), timers=timers,
+                     dist=dist)
+    # synthetic views: random targets, poses on the radius-1.3 sphere
+    g = torch.Generator(device="cpu").manual_seed(99 + rank)
+    n_views = 8
+    gts = [torch.rand(R, 3, generator=g).to(dev) for _ in range(n_views)]
+    poses = [make_pose(1.3, float(torch.rand(1, generator=g)) * 360 - 180,
+                       float(torch.rand(1, generator=g)) * 50 - 10).to(dev) for _ in range(n_views)]
+
+    def step(i):
+        v = i % n_views
+        obj = (i * world + rank) % n_obj
+        core.train_step(H, W, focal, poses[v], gts[v], obj)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timers.on = True
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    samples_per_step = R * (args.n_coarse + args.n_fine)
+    value = samples_per_step * world * args.steps / dt
+    ms = dt / args.steps * 1e3
+
+    kern = timers.summary()
+    peak = BF16_PEAK_TFLOPS if args.precision == "bf16" else FP32_PEAK_TFLOPS
+    roof = None
+    if kern:
+        flops = {k: FLOP_PER_SAMPLE[k] * samples_per_step for k in FLOP_PER_SAMPLE if k in kern}
+        dom = max(flops, key=lambda k: kern[k])
+        achieved = flops[dom] / (kern[dom] * 1e-3) / 1e12
+        roof = {"bound": "mfma", "kernel": {"fwd": "chain_kernel<fwd,train>", "bwd": "chain_kernel<bwd>",
+                                            "dw": "dw_kernel"}[dom],
+                "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4), "traffic": load_traffic(dom),
+                "ms_per_launch": {k: round(v, 4) for k, v in kern.items()}}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_threads)
+
+    if rank == 0:
+        out = {
+            "metric": "ray-samples/sec (train step), SRN-cars 128x128, 64 coarse + 64 fine samples",
+            "value": round(value, 1), "unit": "ray-samples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
+            "data": "synthetic (random 128x128 targets, poses on a radius-1.3 sphere, random-init weights)",
+            "config": {"workload": f"srncar.json net, {H}x{W} image/object/step, {args.n_coarse}+{args.n_fine} "
+                                   f"samples/ray, train step incl. AdamW", "objects_per_step": world,
+                       "rays_per_step_per_gpu": R, "parallelism": f"dp{world}"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def load_traffic(kernel):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3
+    PMC summary (profiles/*pmc*.json), or None."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get(kernel)
+    except OSError:
+        return None
+
+
+def cpu_baseline(threads):
+    """The CPU oracle (torch fp32 restatement of the reference, pinned to its
+    golden vectors) on a bounded sample: a 2048-ray chunk x 128 samples,
+    forward + compositing + MSE + backward, timed on this host's cores."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from oracle import ref_cpu
+    from oracle.params import make_params
+    torch.set_num_threads(threads)
+    p = ref_cpu.param_tensors(make_params(0))
+    s = (torch.randn(1, 256) / 11.3).requires_grad_()
+    t = (torch.randn(1, 256) / 11.3).requires_grad_()
+    B, N = 2048, 128
+    ro = torch.zeros(B, 3) + torch.tensor([0.0, 0.4, 1.2])
+    vd = torch.nn.functional.normalize(torch.randn(B, 3) * 0.2 + torch.tensor([0., -0.3, -1.]), dim=-1)
+    z = torch.linspace(0.8, 1.8, N)
+    gt = torch.rand(B, 3)
+
+    def one():
+        xyz = ro[:, None, :] + vd[:, None, :] * z[:, None]
+        sig, rgb = ref_cpu.codenerf_forward(p, xyz, vd[:, None, :].expand(-1, N, -1), s, t)
+        col, _ = ref_cpu.volume_rendering(sig, rgb, z)
+        ((col - gt) ** 2).mean().backward()
+
+    one()
+    reps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < 10.0 or reps < 2:
+        one()
+        reps += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(B * N * reps / dt, 1), "unit": "ray-samples/s", "cores": threads, "kind": "port",
+            "sample": f"{reps} x (2048 rays x 128 samples) fwd+composite+MSE+backward, torch CPU fp32 oracle"}
+
+
+if __name__ == "__main__":
+    main()

@@ -16,8 +16,9 @@ from . import engine as _eng
 
 
 class ImageStep:
-    def __init__(self, model, chunk=2048, reg_coef=1e-4, white_bg=True):
+    def __init__(self, model, chunk=2048, reg_coef=1e-4, white_bg=True, timers=None):
         self.model = model
+        self.timers = timers
         self.chunk = int(chunk)
         self.reg_coef = float(reg_coef)
         self.white_bg = bool(white_bg)
@@ -59,11 +60,21 @@ class ImageStep:
         eng.ensure_packed(params, bwd=True)
         s, t = shape_table.detach()[obj_idx], texture_table.detach()[obj_idx]
         blob, zvec = eng.latent_fwd(params, s, t)
+        tm = self.timers
+        ev = tm.mark("fwd") if tm else None
         sigma, rgb = eng.mlp_fwd(blob, M, rays_o=rays_o, rays_d=viewdirs, z=z, z_stride=z_stride,
                                  n_samples=N, act=buf["act"])
+        if tm:
+            tm.done("fwd", ev)
         out_rgb, chunk_loss, dsig, drgb = _eng.render_loss(sigma, rgb, z, R, N, gt, self.chunk, self.white_bg)
+        ev = tm.mark("bwd") if tm else None
         eng.mlp_bwd(blob, M, dsig, drgb, buf["act"])
+        if tm:
+            tm.done("bwd", ev)
+            ev = tm.mark("dw")
         eng.mlp_dw(buf["act"], M, zvec, grads, buf["dbuf"], buf["dw"])
+        if tm:
+            tm.done("dw", ev)
         reg_out = torch.zeros(1, dtype=torch.float32, device=eng.device)
         eng.latent_bwd(params, grads, s, t, zvec, buf["dbuf"], shape_table.grad[obj_idx],
                        texture_table.grad[obj_idx], self.reg_coef if reg else 0.0, reg_out)
