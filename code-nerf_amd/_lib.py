@@ -11,7 +11,9 @@ import os
 import torch
 
 LIB_NAME = "libcodenerf_hip.so"
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+# CODENERF_LIB selects another build of the same library (kernel variants
+# built side by side for A/B measurements); it must export the same ABI.
+LIB_PATH = os.environ.get("CODENERF_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 CN_FP32 = 0
 CN_BF16 = 1
@@ -45,7 +47,7 @@ _SIGS = {
     "cn_dw_ws_bytes": (_Z, [_P, _I]),
     "cn_pack_weights": (_I, [_P, _P, _P, _P, _P]),
     "cn_latent_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P]),
-    "cn_mlp_fwd": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P]),
+    "cn_mlp_fwd": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _I, _I, _P]),
     "cn_mlp_bwd": (_I, [_P, _P, _P, _I, _P, _P, _P, _P]),
     "cn_mlp_dw": (_I, [_P, _P, _I, _P, _P, _P, _P, _P]),
     "cn_latent_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P]),
@@ -54,6 +56,9 @@ _SIGS = {
     "cn_composite_fwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P]),
     "cn_composite_bwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
     "cn_render_loss": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P]),
+    "cn_sample_pdf": (_I, [_P, _P, _I, _I, _I, _P, _I, _P, _P]),
+    "cn_render_loss_fine": (_I, [_P, _P, _P, _I, _I, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P,
+                                 _P]),
     "cn_adamw_step": (_I, [_I, _P, _P, _P, _P, _P, _P, _D, _D, _D, _D, _I, _P]),
 }
 

@@ -112,7 +112,8 @@ int cn_latent_fwd(const cn_plan* p, const float* const* d_params, const float* d
 
 int cn_mlp_fwd(const cn_plan* p, const void* d_pack, const float* d_blob, int M, const float* d_xyz,
                const float* d_viewdir, const float* d_rays_o, const float* d_rays_d, const float* d_z,
-               int z_stride, int n_samples, float* d_sigma, float* d_rgb, void* d_act, void* stream) {
+               int z_stride, int n_samples, float* d_sigma, float* d_rgb, void* d_act, int act_M, int act_row0,
+               void* stream) {
   if (!p || !d_pack || !d_blob || !d_sigma || !d_rgb) return fail("cn_mlp_fwd: NULL argument");
   if (M <= 0) return fail("cn_mlp_fwd: M must be positive");
   ChainArgs a{};
@@ -140,14 +141,26 @@ int cn_mlp_fwd(const cn_plan* p, const void* d_pack, const float* d_blob, int M,
   a.rgb = d_rgb;
   const int Mp = cn_pad_samples(p, M);
   if (d_act) {
-    const ActLayout L = p->cs.layout(Mp);
+    // the workspace may be sized for act_M samples, this launch filling rows
+    // [act_row0, act_row0 + Mp) of it (coarse and fine passes share one
+    // workspace, so one backward / dW covers both)
+    if (act_M <= 0) act_M = M;
+    if (act_row0 < 0 || act_row0 % p->cs.tile) return fail("cn_mlp_fwd: act_row0 must be a multiple of the tile");
+    const int Ma = cn_pad_samples(p, act_M);
+    if (act_row0 + Mp > Ma) return fail("cn_mlp_fwd: rows exceed the activation workspace");
+    const ActLayout L = p->cs.layout(Ma);
+    const size_t es = p->cs.prec ? 2 : 4;
+    const size_t r0 = (size_t)act_row0;
     char* b = (char*)d_act;
-    a.pe = b + L.pe;
-    a.dir = b + L.dir;
-    for (int i = 0; i < kMaxPlanes; ++i) { a.Y[i] = b + L.Y[i]; a.dA[i] = b + L.dA[i]; }
-    a.d8 = b + L.d8;
-    a.spre = (float*)(b + L.spre);
-    a.masks = (uint32_t*)(b + L.masks);
+    a.pe = b + L.pe + r0 * 64 * es;
+    a.dir = b + L.dir + r0 * 32 * es;
+    for (int i = 0; i < kMaxPlanes; ++i) {
+      a.Y[i] = b + L.Y[i] + r0 * L.Yw[i] * es;
+      a.dA[i] = b + L.dA[i] + r0 * L.dAw[i] * es;
+    }
+    a.d8 = b + L.d8 + r0 * 32 * es;
+    a.spre = (float*)(b + L.spre) + r0;
+    a.masks = (uint32_t*)(b + L.masks + (r0 / 32) * L.mask_bytes_per_slab);
   }
   const int grid = Mp / p->cs.tile;
   hipLaunchKernelGGL(d_act ? p->cs.fwd_train : p->cs.fwd_infer, dim3(grid), dim3(p->cs.waves * 64), 0,
@@ -185,9 +198,10 @@ int cn_mlp_dw(const cn_plan* p, void* d_act, int M, const float* d_zvec, float* 
   DwArgs dw;
   DwRedArgs red;
   const int nwg = p->cs.dw_setup((char*)d_act, M, d_zvec, d_dbuf, (char*)d_ws, &dw, &red);
+  if (nwg <= 0) return fail("cn_mlp_dw: schedule does not fit the partial workspace");
   red.grads = d_grads;
-  if (p->cs.prec) hipLaunchKernelGGL(dw_kernel<CN_P_BF16>, dim3(nwg), dim3(256), 0, S(stream), dw);
-  else hipLaunchKernelGGL(dw_kernel<CN_P_FP32>, dim3(nwg), dim3(256), 0, S(stream), dw);
+  if (p->cs.prec) hipLaunchKernelGGL(dw_kernel<CN_P_BF16>, dim3(nwg), dim3(512), 0, S(stream), dw);
+  else hipLaunchKernelGGL(dw_kernel<CN_P_FP32>, dim3(nwg), dim3(512), 0, S(stream), dw);
   if (launch_check("dw_kernel")) return -1;
   hipLaunchKernelGGL(dw_reduce_kernel, dim3(grid_for(red.prefix[red.nprob], 256)), dim3(256), 0, S(stream), red);
   return launch_check("dw_reduce_kernel");
@@ -256,6 +270,39 @@ int cn_render_loss(const float* d_sigma, const float* d_rgb, const float* d_z, i
   hipLaunchKernelGGL(render_loss_kernel, dim3(grid_for(R, 4)), dim3(256), 0, S(stream), d_sigma, d_rgb, d_z,
                      z_stride, R, N, white_bg, d_gt, chunk, d_out_rgb, d_ray_se, d_dsig, d_drgb);
   if (launch_check("render_loss_kernel")) return -1;
+  hipLaunchKernelGGL(chunk_loss_kernel, dim3(grid_for(R, chunk)), dim3(256), 0, S(stream), d_ray_se, R, chunk,
+                     d_chunk_loss);
+  return launch_check("chunk_loss_kernel");
+}
+
+int cn_sample_pdf(const float* d_sigma_c, const float* d_z_c, int zc_stride, int R, int Nc, const float* d_rand,
+                  int Nf, float* d_z_f, void* stream) {
+  if (!d_sigma_c || !d_z_c || !d_rand || !d_z_f) return fail("cn_sample_pdf: NULL argument");
+  if (check_rn(R, Nc, "cn_sample_pdf")) return -1;
+  if (Nc < 3) return fail("cn_sample_pdf: need at least 3 coarse samples");
+  if (Nf <= 0) return fail("cn_sample_pdf: Nf must be positive");
+  if (zc_stride != 0 && zc_stride != Nc) return fail("cn_sample_pdf: zc_stride must be 0 or Nc");
+  hipLaunchKernelGGL(sample_pdf_kernel, dim3(grid_for(R, 4)), dim3(256), 0, S(stream), d_sigma_c, d_z_c, zc_stride,
+                     R, Nc, d_rand, Nf, d_z_f);
+  return launch_check("sample_pdf_kernel");
+}
+
+int cn_render_loss_fine(const float* d_sigma_c, const float* d_rgb_c, const float* d_z_c, int zc_stride, int Nc,
+                        const float* d_sigma_f, const float* d_rgb_f, const float* d_z_f, int Nf, int R,
+                        int white_bg, const float* d_gt, int chunk, float* d_out_rgb, float* d_ray_se,
+                        float* d_chunk_loss, float* d_dsig_c, float* d_drgb_c, float* d_dsig_f, float* d_drgb_f,
+                        void* stream) {
+  if (!d_sigma_c || !d_rgb_c || !d_z_c || !d_sigma_f || !d_rgb_f || !d_z_f || !d_gt || !d_out_rgb || !d_ray_se ||
+      !d_chunk_loss || !d_dsig_c || !d_drgb_c || !d_dsig_f || !d_drgb_f)
+    return fail("cn_render_loss_fine: NULL argument");
+  if (Nc <= 0 || Nf <= 0) return fail("cn_render_loss_fine: Nc and Nf must be positive");
+  if (check_rn(R, Nc + Nf, "cn_render_loss_fine")) return -1;
+  if (zc_stride != 0 && zc_stride != Nc) return fail("cn_render_loss_fine: zc_stride must be 0 or Nc");
+  if (chunk <= 0) return fail("cn_render_loss_fine: chunk must be positive");
+  hipLaunchKernelGGL(fine_render_loss_kernel, dim3(grid_for(R, 4)), dim3(256), 0, S(stream), d_sigma_c, d_rgb_c,
+                     d_z_c, zc_stride, Nc, d_sigma_f, d_rgb_f, d_z_f, Nf, R, white_bg, d_gt, chunk, d_out_rgb,
+                     d_ray_se, d_dsig_c, d_drgb_c, d_dsig_f, d_drgb_f);
+  if (launch_check("fine_render_loss_kernel")) return -1;
   hipLaunchKernelGGL(chunk_loss_kernel, dim3(grid_for(R, chunk)), dim3(256), 0, S(stream), d_ray_se, R, chunk,
                      d_chunk_loss);
   return launch_check("chunk_loss_kernel");

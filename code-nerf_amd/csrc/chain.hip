@@ -55,6 +55,22 @@ CN_DEV uint32_t push_sign(uint32_t bits, float v) {
   return __builtin_amdgcn_alignbit(bits, __builtin_bit_cast(uint32_t, v), 31);
 }
 
+// Store of 4 consecutive plane elements (group g of feature tile t) of this
+// lane's sample into the wave-tiled plane layout (cn_layout.h): the per-lane
+// part of the address is voff[g] (precomputed), the rest is wave-uniform.
+template <class E>
+CN_DEV void plane_store(__amdgpu_buffer_rsrc_t r, const uint32_t* voff, int F, int wglob, int t, int g,
+                        float a, float b, float c, float d) {
+  const int soff = ((wglob * (F >> 5) + t) * 4 + g) * (256 * (int)sizeof(E));
+  bstore4<E>(r, voff[g], soff, a, b, c, d);
+}
+template <class E>
+CN_DEV void plane_store_packed(__amdgpu_buffer_rsrc_t r, const uint32_t* voff, int F, int wglob, int t, int g,
+                               u32x2 v) {
+  const int soff = ((wglob * (F >> 5) + t) * 4 + g) * (256 * (int)sizeof(E));
+  bstore64(r, voff[g], v, soff);
+}
+
 template <int P, int SB, int TB, bool BWD, int WAVES, bool TRAIN>
 struct Chain {
   using S = Sched<P, SB, TB, BWD>;
@@ -124,6 +140,9 @@ struct Chain {
     const int mc = m < a.M ? m : a.M - 1;
     const int wglob = blockIdx.x * WAVES + w;
     float* prm = (float*)(smem + kRingBytes);
+    uint32_t voff[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) voff[g] = (uint32_t)tile_pos(lane & 31, g, h) * (4 * sizeof(E));
 
     // -- per-call bias blob -> LDS (plain loads; nothing is in flight yet)
     for (int i = threadIdx.x; i < kBlobFloats / 4; i += WAVES * 64)
@@ -138,9 +157,9 @@ struct Chain {
 
     float ds = 0.f;   // bwd: sigma-head pre-activation gradient of this sample
     if constexpr (!BWD) {
-      prologue_fwd(a, bin, smem, h, lane, w, m, mc);
+      prologue_fwd(a, bin, smem, h, lane, w, m, mc, wglob, voff);
     } else {
-      ds = prologue_bwd(a, bin, smem, h, lane, w, m, mc, wglob);
+      ds = prologue_bwd(a, bin, smem, h, lane, w, m, mc, wglob, voff);
     }
     __syncthreads();
     if constexpr (!BWD) load_bias<0>(acc, prm, h);
@@ -175,9 +194,9 @@ struct Chain {
           }
           if constexpr (g == S::last_block(li)) {
             if constexpr (!BWD)
-              epilogue_fwd<li>(a, bin, acc, prm, smem, h, lane, w, m, wglob, sig_part);
+              epilogue_fwd<li>(a, bin, acc, prm, smem, h, lane, w, m, wglob, voff, sig_part);
             else
-              epilogue_bwd<li>(a, bin, acc, prm, smem, h, lane, w, m, ds);
+              epilogue_bwd<li>(a, bin, acc, prm, smem, h, lane, w, m, wglob, voff, ds);
           }
         }
       });
@@ -212,7 +231,7 @@ struct Chain {
 
   // ---------------- prologues
   __device__ static void prologue_fwd(const ChainArgs& a, BinT* bin, char* smem, int h, int lane,
-                                      int w, int m, int mc) {
+                                      int w, int m, int mc, int wglob, const uint32_t* voff) {
     float x[3], d[3];
     if (a.mode == 0) {
       for (int k = 0; k < 3; ++k) { x[k] = a.xyz[3 * mc + k]; d[k] = a.vdir[3 * mc + k]; }
@@ -273,24 +292,31 @@ struct Chain {
         ((f32x4*)stash)[q] = f32x4{dp[4 * q], dp[4 * q + 1], dp[4 * q + 2], dp[4 * q + 3]};
     }
     if constexpr (TRAIN) {
+      // slot q of lane half h -> column slot_col(h, q): group k = q / 4 lands in
+      // feature tile k / 4, group k % 4 (cn_layout.h)
       const auto rp = mkrsrc(a.pe);
-      const uint32_t op = ((uint32_t)m * 64 + h * 32) * sizeof(E);
 #pragma unroll
-      for (int q = 0; q < 32; q += 4) bstore4<E>(rp, op, q * sizeof(E), pe[q], pe[q + 1], pe[q + 2], pe[q + 3]);
+      for (int k = 0; k < 8; ++k)
+        plane_store<E>(rp, voff, 64, wglob, k >> 2, k & 3, pe[4 * k], pe[4 * k + 1], pe[4 * k + 2], pe[4 * k + 3]);
       const auto rd = mkrsrc(a.dir);
-      const uint32_t od = ((uint32_t)m * 32 + h * 16) * sizeof(E);
 #pragma unroll
-      for (int q = 0; q < 16; q += 4) bstore4<E>(rd, od, q * sizeof(E), dp[q], dp[q + 1], dp[q + 2], dp[q + 3]);
+      for (int k = 0; k < 4; ++k)
+        plane_store<E>(rd, voff, 32, wglob, 0, k, dp[4 * k], dp[4 * k + 1], dp[4 * k + 2], dp[4 * k + 3]);
     }
   }
 
   __device__ static float prologue_bwd(const ChainArgs& a, BinT* bin, char* smem, int h, int lane,
-                                       int w, int m, int mc, int wglob) {
-    const float g0 = a.drgb[3 * mc + 0], g1 = a.drgb[3 * mc + 1], g2 = a.drgb[3 * mc + 2];
+                                       int w, int m, int mc, int wglob, const uint32_t* voff) {
+    // padding samples (m >= M) get zero upstream gradients, so every dA they
+    // write is exactly 0 and the dW pass can sum whole 32-sample tiles
+    const bool valid = m < a.M;
+    const float g0 = valid ? a.drgb[3 * mc + 0] : 0.f;
+    const float g1 = valid ? a.drgb[3 * mc + 1] : 0.f;
+    const float g2 = valid ? a.drgb[3 * mc + 2] : 0.f;
     // Softplus backward exactly as torch: grad * (x > 20 ? 1 : e^x / (e^x + 1))
     const float s = a.spre[mc];
     const float ex = expf(s);
-    const float ds = a.dsigma[mc] * (s > 20.f ? 1.f : ex / (ex + 1.f));
+    const float ds = valid ? a.dsigma[mc] * (s > 20.f ? 1.f : ex / (ex + 1.f)) : 0.f;
     if constexpr (kBf16) {
       // k-step 0, lane half h, element j -> drgb component 8h + j
       if (h == 0) bin[0] = u32x4{pack_bf16x2(g0, g1), pack_bf16x2(g2, 0.f), 0u, 0u};
@@ -300,21 +326,20 @@ struct Chain {
       bin[1] = h ? 0.f : g2;
     }
     {
-      // drgb as a padded [M][32] plane for the rgb-head weight gradient
+      // drgb as a padded 32-wide plane for the rgb-head weight gradient
+      // (columns slot_col(0, 0..2) = 0..2)
       const auto r8 = mkrsrc(a.d8);
-      const uint32_t o8 = ((uint32_t)m * 32 + h * 16) * sizeof(E);
-      bstore4<E>(r8, o8, 0, h ? 0.f : g0, h ? 0.f : g1, h ? 0.f : g2, 0.f);
+      plane_store<E>(r8, voff, 32, wglob, 0, 0, h ? 0.f : g0, h ? 0.f : g1, h ? 0.f : g2, 0.f);
 #pragma unroll
-      for (int q = 4; q < 16; q += 4) bstore4<E>(r8, o8, q * sizeof(E), 0.f, 0.f, 0.f, 0.f);
+      for (int k = 1; k < 4; ++k) plane_store<E>(r8, voff, 32, wglob, 0, k, 0.f, 0.f, 0.f, 0.f);
       // the sigma-head gradient rides in columns 256 (value) and 257 (its
       // rounding residual, so bf16 storage keeps ~16 significant bits) of the
-      // viewdir dA plane
+      // viewdir dA plane (feature tile 8 of its 288 columns)
       const auto rv = mkrsrc(a.dA[SB + 2]);
-      const uint32_t ov = ((uint32_t)m * 288 + 256 + h * 16) * sizeof(E);
       const float ds_hi = (float)(E)ds;
-      bstore4<E>(rv, ov, 0, h ? 0.f : ds_hi, h ? 0.f : ds - ds_hi, 0.f, 0.f);
+      plane_store<E>(rv, voff, 288, wglob, 8, 0, h ? 0.f : ds_hi, h ? 0.f : ds - ds_hi, 0.f, 0.f);
 #pragma unroll
-      for (int q = 4; q < 16; q += 4) bstore4<E>(rv, ov, q * sizeof(E), 0.f, 0.f, 0.f, 0.f);
+      for (int k = 1; k < 4; ++k) plane_store<E>(rv, voff, 288, wglob, 8, k, 0.f, 0.f, 0.f, 0.f);
     }
     // ReLU sign bits of this wave -> LDS
     const u32x4* src = (const u32x4*)a.masks + (size_t)wglob * N::kMasks * 64 + lane;
@@ -328,7 +353,7 @@ struct Chain {
   template <int LI>
   __device__ static void epilogue_fwd(const ChainArgs& a, BinT* bin, f32x16* acc, const float* prm,
                                       const char* smem, int h, int lane, int w, int m, int wglob,
-                                      float& sig_part) {
+                                      const uint32_t* voff, float& sig_part) {
     constexpr Layer l = S::L(LI);
     if constexpr (l.epi == EPI_RGB) {
       if (h == 0) {
@@ -340,8 +365,8 @@ struct Chain {
     } else {
       uint32_t mbits[4] = {0u, 0u, 0u, 0u};
       constexpr int yp = l.plane >= 0 ? l.plane : 0;
+      constexpr int YF = N::plane_width(yp);
       const auto ry = mkrsrc(a.Y[yp]);
-      const uint32_t oy = ((uint32_t)m * N::plane_width(yp) + 4 * h) * sizeof(E);
       const float* ws = prm + kWsOff + 4 * h;
 #pragma unroll
       for (int t = 0; t < l.T; ++t) {
@@ -369,7 +394,7 @@ struct Chain {
             BinT& b = bin[2 * t + (g >> 1)];
             if ((g & 1) == 0) { b[0] = p0; b[1] = p1; } else { b[2] = p0; b[3] = p1; }
             if constexpr (TRAIN && l.plane >= 0)
-              bstore64(ry, oy, u32x2{p0, p1}, (32 * t + 8 * g) * 2);
+              plane_store_packed<E>(ry, voff, YF, wglob, t, g, u32x2{p0, p1});
           } else {
             if constexpr (l.epi == EPI_RELU) {
               v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
@@ -379,7 +404,7 @@ struct Chain {
             bin[16 * t + 4 * g + 2] = v2;
             bin[16 * t + 4 * g + 3] = v3;
             if constexpr (TRAIN && l.plane >= 0)
-              bstore128(ry, oy, u32x4{f2u(v0), f2u(v1), f2u(v2), f2u(v3)}, (32 * t + 8 * g) * 4);
+              plane_store<E>(ry, voff, YF, wglob, t, g, v0, v1, v2, v3);
           }
         }
       }
@@ -416,11 +441,11 @@ struct Chain {
 
   template <int LI>
   __device__ static void epilogue_bwd(const ChainArgs& a, BinT* bin, f32x16* acc, const float* prm,
-                                      const char* smem, int h, int lane, int w, int m, float ds) {
+                                      const char* smem, int h, int lane, int w, int m, int wglob,
+                                      const uint32_t* voff, float ds) {
     constexpr Layer l = S::L(LI);
     constexpr int width = N::dplane_width(l.plane);
     const auto rdA = mkrsrc(a.dA[l.plane]);
-    const uint32_t odA = ((uint32_t)m * width + 4 * h) * sizeof(E);
     u32x4 mw = u32x4{0u, 0u, 0u, 0u};
     if constexpr (l.epi == EPI_BMASK)
       mw = *(const u32x4*)(smem + kMaskOff + (((size_t)w * N::kMasks + l.mask) * 64 + lane) * 16);
@@ -450,11 +475,11 @@ struct Chain {
           const uint32_t p0 = pack_bf16x2(v[0], v[1]), p1 = pack_bf16x2(v[2], v[3]);
           BinT& b = bin[2 * t + (g >> 1)];
           if ((g & 1) == 0) { b[0] = p0; b[1] = p1; } else { b[2] = p0; b[3] = p1; }
-          bstore64(rdA, odA, u32x2{p0, p1}, (32 * t + 8 * g) * 2);
+          plane_store_packed<E>(rdA, voff, width, wglob, t, g, u32x2{p0, p1});
         } else {
 #pragma unroll
           for (int i = 0; i < 4; ++i) bin[16 * t + 4 * g + i] = v[i];
-          bstore128(rdA, odA, u32x4{f2u(v[0]), f2u(v[1]), f2u(v[2]), f2u(v[3])}, (32 * t + 8 * g) * 4);
+          plane_store<E>(rdA, voff, width, wglob, t, g, v[0], v[1], v[2], v[3]);
         }
       }
       acc[t] = f32x16{};

@@ -15,6 +15,8 @@ struct LatentBwdArgs;
 
 struct ActLayout {
   size_t pe = 0, dir = 0, Y[kMaxPlanes] = {}, dA[kMaxPlanes] = {}, d8 = 0, spre = 0, masks = 0, bytes = 0;
+  size_t Yw[kMaxPlanes] = {}, dAw[kMaxPlanes] = {};   // plane widths (elements per sample)
+  size_t mask_bytes_per_slab = 0;                     // per 32-sample slab
 };
 
 struct ChainSet {

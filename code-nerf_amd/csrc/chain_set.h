@@ -81,95 +81,69 @@ ActLayout act_layout(size_t Mp) {
   auto take = [&](size_t n) { size_t o = off; off += (n + 255) & ~(size_t)255; return o; };
   L.pe = take(Mp * 64 * es);
   L.dir = take(Mp * 32 * es);
-  for (int p = 0; p < N::kPlanes; ++p) L.Y[p] = take(Mp * N::plane_width(p) * es);
-  for (int p = 0; p < N::kPlanes; ++p) L.dA[p] = take(Mp * N::dplane_width(p) * es);
+  for (int p = 0; p < N::kPlanes; ++p) {
+    L.Yw[p] = N::plane_width(p);
+    L.Y[p] = take(Mp * L.Yw[p] * es);
+  }
+  for (int p = 0; p < N::kPlanes; ++p) {
+    L.dAw[p] = N::dplane_width(p);
+    L.dA[p] = take(Mp * L.dAw[p] * es);
+  }
   L.d8 = take(Mp * 32 * es);
   L.spre = take(Mp * 4);
-  L.masks = take(Mp / 32 * N::kMasks * 64 * 16);
+  L.mask_bytes_per_slab = (size_t)N::kMasks * 64 * 16;
+  L.masks = take(Mp / 32 * L.mask_bytes_per_slab);
   L.bytes = off;
   return L;
 }
 
-// dW job geometry for M samples: slices and per-problem tile counts
-template <int SB, int TB>
-struct DwGeom {
-  using N = Net<SB, TB>;
-  static constexpr int NP = N::kFwdLayers;
-  int out_valid[NP], in_valid[NP], out_tiles[NP], in_tiles[NP];
-  int tiles = 0, slices = 1, mchunk = 32;
-  DwGeom(int M) {
-    for (int L = 0; L < NP; ++L) {
-      const bool last = L == NP - 1;
-      out_valid[L] = last ? 3 : (L == SB + 2 ? 258 : N::dplane_width(L));
-      in_valid[L] = L == 0 ? 64 : (L == SB + 2 ? 288 : (last ? 128 : 256));
-      out_tiles[L] = (out_valid[L] + 127) / 128;
-      in_tiles[L] = (in_valid[L] + 127) / 128;
-      tiles += out_tiles[L] * in_tiles[L];
-    }
-    const int steps = std::max(1, (M + 31) / 32);
-    slices = std::max(1, std::min(std::min(16, steps), (512 + tiles - 1) / tiles));
-    mchunk = ((steps + slices - 1) / slices) * 32;
-    slices = std::max(1, (M + mchunk - 1) / mchunk);
-  }
-  size_t part_floats(int L) const { return (size_t)slices * out_tiles[L] * 128 * in_tiles[L] * 128; }
-  size_t db_floats(int L) const { return (size_t)slices * out_tiles[L] * 128; }
-  size_t ws_bytes() const {
-    size_t s = 0;
-    for (int L = 0; L < NP; ++L) s += (part_floats(L) + db_floats(L)) * 4 + 512;
-    return s;
-  }
-};
+// dW schedule for M samples: kDwWorkgroups persistent workgroups (one per CU)
+// each take an equal byte share of the (layer, slab) stream.
+constexpr int kDwWorkgroups = 256;
 
 template <int P, int SB, int TB>
-size_t dw_ws_bytes(int M) { return DwGeom<SB, TB>(M).ws_bytes(); }
+size_t dw_ws_bytes(int) {
+  return (size_t)kDwWorkgroups * 2 * ((size_t)kPartRows * kPartCols + kPartRows) * sizeof(float);
+}
 
 template <int P, int SB, int TB>
 int dw_setup(char* act, int M, const float* zvec, float* dbuf, char* ws, DwArgs* dw, DwRedArgs* red) {
   using N = Net<SB, TB>;
   constexpr ParamIdx PI{SB, TB};
-  const DwGeom<SB, TB> G(M);
+  constexpr int ES = P == CN_P_BF16 ? 2 : 4;
   const int Mp = ((M + 255) / 256) * 256;
   const ActLayout A = act_layout<P, SB, TB>(Mp);
   static_assert(N::kFwdLayers <= kDwMaxProblems, "dw problems");
   *dw = DwArgs{};
   *red = DwRedArgs{};
   dw->nprob = red->nprob = N::kFwdLayers;
-  dw->M = M;
-  dw->slices = red->slices = G.slices;
-  dw->mchunk = G.mchunk;
-  size_t off = 0;
-  int tp = 0, ep = 0;
+  dw->total_tiles = Mp / 32;
+  int ep = 0;
+  long long wsum = 0, min_total = -1;
   for (int L = 0; L < N::kFwdLayers; ++L) {
     const bool last = L == N::kFwdLayers - 1;
+    const bool vd = L == SB + 2;
     DwProblem& p = dw->p[L];
     p.A = act + (last ? A.d8 : A.dA[L]);
-    p.lda = last ? 32 : N::dplane_width(L);
-    p.a_valid = G.out_valid[L];
-    if (L == 0) { p.X0 = act + A.pe; p.ldx0 = 64; p.x0_cols = 64; }
-    else if (L == SB + 2) {
-      p.X0 = act + A.Y[SB + 1]; p.ldx0 = 256; p.x0_cols = 256;
-      p.X1 = act + A.dir; p.ldx1 = 32;
-    } else { p.X0 = act + A.Y[L - 1]; p.ldx0 = N::plane_width(L - 1); p.x0_cols = p.ldx0; }
-    if (!p.X1) { p.X1 = p.X0; p.ldx1 = p.ldx0; }
-    p.in_valid = G.in_valid[L];
-    p.out_tiles = G.out_tiles[L];
-    p.in_tiles = G.in_tiles[L];
-    p.part = (float*)(ws + off);
-    off += ((G.part_floats(L) * 4 + 255) & ~(size_t)255);
-    p.dbpart = (float*)(ws + off);
-    off += ((G.db_floats(L) * 4 + 255) & ~(size_t)255);
-    dw->tile_prefix[L] = tp;
-    tp += p.out_tiles * p.in_tiles;
+    p.a_width = last ? 32 : N::dplane_width(L);
+    p.a_tiles = p.a_width / 32;
+    p.out_tiles = last ? 1 : N::fwd(L).T;
+    if (L == 0) { p.X0 = act + A.pe; p.x0_width = 64; }
+    else { p.X0 = act + A.Y[L - 1]; p.x0_width = N::plane_width(L - 1); }
+    p.x0_tiles = p.x0_width / 32;
+    if (vd) { p.X1 = act + A.dir; p.x1_width = 32; p.x1_tiles = 1; }
+    p.sigma_head = vd ? 1 : 0;
+    dw->pbytes[L] = (p.a_tiles + p.x0_tiles + p.x1_tiles) * 1024 * ES;
+    dw->wprefix[L] = wsum;
+    const long long tot = (long long)dw->pbytes[L] * dw->total_tiles;
+    wsum += tot;
+    if (min_total < 0 || tot < min_total) min_total = tot;
 
     DwRedProblem& r = red->p[L];
-    r.part = p.part;
-    r.dbpart = p.dbpart;
-    r.ldp = p.in_tiles * 128;
-    r.rows_pad = p.out_tiles * 128;
     r.out_real = last ? 3 : N::fwd(L).T * 32;
     r.in_real = real_in_width<SB>(L, TB);
-    r.cols = p.in_valid;
-    r.map = L == 0 ? MAP_PE : (L == SB + 2 ? MAP_VIEWDIR : MAP_PLAIN);
+    r.cols = (p.x0_tiles + p.x1_tiles) * 32;
+    r.map = L == 0 ? MAP_PE : (vd ? MAP_VIEWDIR : MAP_PLAIN);
     r.w = N::fwd(L).w;
     r.b = N::fwd(L).b;
     r.w2 = PI.sigma_w();
@@ -177,13 +151,24 @@ int dw_setup(char* act, int M, const float* zvec, float* dbuf, char* ws, DwArgs*
     const int inj = L >= 1 ? N::fwd(L - 1).inj : -1;
     r.z = inj >= 0 ? zvec + inj * 256 : nullptr;
     r.dbout = inj >= 0 ? dbuf + inj * 256 : nullptr;
-    r.elems = (r.out_real + (L == SB + 2 ? 2 : 0)) * r.cols;
+    r.elems = (r.out_real + (vd ? 1 : 0)) * r.cols;
+    r.pbytes = dw->pbytes[L];
     red->prefix[L] = ep;
     ep += r.elems;
+    red->wprefix[L] = dw->wprefix[L];
   }
-  dw->tile_prefix[N::kFwdLayers] = tp;
+  dw->wprefix[N::kFwdLayers] = red->wprefix[N::kFwdLayers] = wsum;
   red->prefix[N::kFwdLayers] = ep;
-  return tp * G.slices;
+  // a share (wsum / nwg bytes) never exceeds the smallest problem, so it
+  // holds slabs of at most two problems
+  const long long nwg = kDwWorkgroups;
+  if ((wsum + min_total - 1) / min_total >= nwg) return -1;
+  dw->nwg = red->nwg = (int)nwg;
+  dw->part = (float*)ws;
+  dw->dbpart = (float*)(ws + (size_t)kDwWorkgroups * 2 * kPartRows * kPartCols * sizeof(float));
+  red->part = dw->part;
+  red->dbpart = dw->dbpart;
+  return (int)nwg;
 }
 
 template <int P, int SB, int TB>

@@ -36,6 +36,16 @@ CN_DEV void glds16(const void* gsrc, lds_void* ldst) {
   __builtin_amdgcn_global_load_lds(gsrc, ldst, 16, 0, 0);
 }
 
+// The same LDS-DMA as opaque asm.  The compiler then does not know the
+// instruction writes LDS, so it does not drain every DMA in flight before
+// each LDS read it cannot prove disjoint (it cannot, when the read comes from
+// a ds_read_tr builtin, whose memory operand carries no alias scope); the
+// caller owns the vmcnt bookkeeping (wait_vmcnt) entirely.
+CN_DEV void glds16_opaque(const void* gsrc, uint32_t lds_byte) {
+  asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "{m0}"(lds_byte) : "memory");
+}
+CN_DEV uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)(lds_void*)p; }
+
 template <int N>
 CN_DEV void wait_vmcnt() {
   static_assert(N >= 0, "vmcnt");

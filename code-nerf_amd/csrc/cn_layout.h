@@ -158,4 +158,29 @@ inline constexpr int f32_acc_feature(int q, int h) {
 // accumulator register r of lane half h -> row within the 32-row tile
 inline constexpr int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
+// ---- activation planes in HBM: wave-tiled, bank-swizzled --------------------
+// A plane of width F (multiple of 32) over Mp samples is stored per 32-sample
+// wave tile w, per 32-feature tile t, per 8-feature group g as 64 "positions"
+// of 4 consecutive features (8 B bf16 / 16 B fp32).  The position of sample s
+// (0..31) and feature half hh = (f >> 2) & 1 is
+//     pos = ((s + 8 g + 4 hh) & 31) + 32 hh,
+// i.e. the lanes of one epilogue store instruction (lane = s + 32 h writes
+// features 32t + 8g + 4h .. +3) fill one contiguous 64 x 4-element block, and a
+// 32-sample x F slab is one contiguous F*32*es-byte run.  The rotation by
+// 8g + 4hh makes the transposed LDS reads of the dW kernel (4 samples x 4
+// features per lane, 32 lanes spanning 4 samples x 32 features) hit 64
+// distinct banks.
+inline constexpr int tile_pos(int s, int g, int hh) { return ((s + 8 * g + 4 * hh) & 31) + 32 * hh; }
+// byte offset of features f .. f+3 (f % 4 == 0) of sample m
+inline constexpr uint64_t plane_off(uint64_t m, int f, int F, int es) {
+  return (((m >> 5) * (uint64_t)(F >> 5) + (uint64_t)(f >> 5)) * 4 + (uint64_t)((f >> 3) & 3)) * (256u * es) +
+         (uint64_t)tile_pos((int)(m & 31), (f >> 3) & 3, (f >> 2) & 1) * (4u * es);
+}
+// prologue planes (PE, dir, drgb, sigma-head columns): the q-th value a lane
+// half h holds goes to column 8 (q / 4) + 4 h + (q % 4), so it is written by the
+// same store pattern as an epilogue group.
+inline constexpr int slot_col(int h, int q) { return 8 * (q >> 2) + 4 * h + (q & 3); }
+inline constexpr int col_half(int c) { return (c >> 2) & 1; }
+inline constexpr int col_slot(int c) { return 4 * (c >> 3) + (c & 3); }
+
 }  // namespace cn

@@ -1,19 +1,21 @@
 // Weight gradients of the CodeNeRF MLP: dW_L = sum_m dA_L[m] (x) X_L[m].
 //
-// The reduction runs over samples (K = M, ~1e6), so each workgroup owns one
-// 128 x 128 output tile of one layer over one slice of the samples and writes
-// an fp32 partial; dw_reduce sums the slices (deterministic, no atomics),
-// maps padded / permuted columns back to the reference tensors, adds the
-// code-injection correction db (x) z (the forward folds y + z into the bias)
-// and accumulates into .grad.  Bias gradients (row sums of dA) are computed in
-// the same pass from the A fragments.
-//
-// Operands are sample-major planes written by the chain kernels.  A 32-sample
-// slab of each operand is staged through LDS (register staging, double
-// buffered) and read back transposed:
-//   bf16: ds_read_b64_tr_b16 (4 samples x 1 feature per lane per read) feeding
+// The reduction runs over samples (K = M ~ 1e6): a workgroup owns the WHOLE
+// (<= 256 x 288) gradient of one layer over one slice of the samples, so each
+// operand byte is read from HBM exactly once (this pass is HBM-bound: ~7.7 KB
+// of bf16 operands per sample against 0.9 MFLOP).  Every 32-sample slab of an
+// operand is one contiguous run in the wave-tiled plane layout (cn_layout.h);
+// it is staged through registers into a double-buffered LDS image that keeps
+// the HBM layout, and read back transposed:
+//   bf16: ds_read_b64_tr_b16 (4 samples x 1 feature per lane per read; the
+//         layout's rotation makes the reads bank-conflict free) feeding
 //         v_mfma_f32_32x32x16_bf16 with K = samples;
 //   fp32: ds_read_b32 feeding v_mfma_f32_32x32x2_f32 (exact fp32).
+// Bias gradients (row sums of dA) come from the A fragments; the sigma head
+// (ds x y_shape, 1 x 256) is a VALU side-product of the viewdir job.  Slices
+// write fp32 partials; dw_reduce sums them (deterministic, no atomics), maps
+// padded / permuted columns back to the reference tensors, adds the
+// code-injection correction db (x) z and accumulates into .grad.
 #include "cn_common.h"
 #include "chain_args.h"
 #include "dw_args.h"
@@ -24,186 +26,275 @@ template <int P>
 struct DwCfg;
 template <> struct DwCfg<CN_P_BF16> {
   using E = __bf16;
-  static constexpr int kRow = 128 * 2 + 64;     // padded LDS row bytes (conflict-free tr reads)
-  static constexpr int kPieces = 2;             // 16-byte pieces per thread per tile
+  static constexpr int kLoads = 5;      // 16-byte pieces per thread per slab (<= 18 x 2 KiB)
 };
 template <> struct DwCfg<CN_P_FP32> {
   using E = float;
-  static constexpr int kRow = 128 * 4;
-  static constexpr int kPieces = 4;
+  static constexpr int kLoads = 9;      // <= 18 x 4 KiB
 };
 
 typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
+template <int ES>
+CN_DEV int img_off(int s, int f) {
+  // byte offset, inside a staged slab image, of features f..f+3 of sample s
+  return (f >> 5) * (1024 * ES) + ((f >> 3) & 3) * (256 * ES) + tile_pos(s, (f >> 3) & 3, (f >> 2) & 1) * (4 * ES);
+}
+
+// One segment: the slabs [t0, t1) of one problem, accumulated into a partial.
 template <int P>
-__global__ __launch_bounds__(256, 2) void dw_kernel(DwArgs a) {
+struct DwSeg {
   using C = DwCfg<P>;
   using E = typename C::E;
-  constexpr bool kBf16 = P == CN_P_BF16;
-  constexpr int kTile = 32 * C::kRow;            // one 32-sample x 128-feature slab
-  constexpr int kEPP = 16 / sizeof(E);           // elements per 16-byte piece
-  constexpr int kPPR = 128 / kEPP;               // pieces per row
-  __shared__ __attribute__((aligned(16))) char smem[4 * kTile];   // [buf][A|X]
+  static constexpr bool kBf16 = P == CN_P_BF16;
+  static constexpr int ES = sizeof(E);
+  static constexpr int kTileB = 1024 * ES;                // one 32-sample x 32-feature tile
+  static constexpr int kStage = 18 * kTileB;              // A (<= 9 tiles) + X (<= 9 tiles)
+#ifndef CN_DW_DEPTH
+#define CN_DW_DEPTH 2
+#endif
+  static constexpr int kDepth = CN_DW_DEPTH;              // bf16: slabs in flight
+  static constexpr int kG = 5;                            // 8 waves x 5 KiB = 40 KiB >= 36 KiB
+  static constexpr int kRingStage = 8 * kG * 1024;
+  static constexpr int kSmem = kBf16 ? (kDepth + 1) * kRingStage : 2 * kStage;
 
-  // ---- job decode: problem, output tile, input tile, sample slice
-  const int tiles_total = a.tile_prefix[a.nprob];
-  const int job = blockIdx.x;
-  const int slice = job / tiles_total;
-  int rem = job - slice * tiles_total;
-  int pi = 0;
-  while (pi + 1 < a.nprob && a.tile_prefix[pi + 1] <= rem) ++pi;
-  rem -= a.tile_prefix[pi];
-  const DwProblem& pr = a.p[pi];
-  const int to = rem / pr.in_tiles, ti = rem % pr.in_tiles;
-  const int m0 = slice * a.mchunk;
-  const int m1 = min(a.M, m0 + a.mchunk);
+  __device__ static void run(const DwProblem& pr, int t0, int t1, int rot, float* part, float* dbpart,
+                             char* smem) {
+    const int nst = t1 - t0;
+    // slab visited at step st: rotated so that the workgroups streaming one
+    // plane do not walk it in lockstep at a power-of-two stride (HBM channel
+    // camping); the sum does not depend on the order.
+    rot %= nst;
+    auto slab = [&](int st) { const int t = st + rot; return t0 + (t >= nst ? t - nst : t); };
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wo = w >> 1, wi = w & 1;           // rows 64*wo.., cols 128*wi..
+    const int h = lane >> 5;
+    const int xt = pr.x0_tiles + pr.x1_tiles;    // staged X feature tiles
+    const bool extra = (wi == 0) && xt > 8;      // 9th X tile (dir PE) on the wi == 0 waves
+    const int a_bytes = pr.a_tiles * kTileB, x0_bytes = pr.x0_tiles * kTileB, x1_bytes = pr.x1_tiles * kTileB;
+    const int stage_pieces = (a_bytes + x0_bytes + x1_bytes) >> 4;
+    const bool row0_live = 64 * wo < pr.out_tiles * 32;
+    const bool row1_live = 64 * wo + 32 < pr.out_tiles * 32;
+    const bool cols_live = 128 * wi < min(xt, 8) * 32;
+    const bool live = row0_live && (cols_live || extra);
 
-  const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
-  const int wo = w >> 1, wi = w & 1;   // wave sub-tile: rows 64*wo, cols 64*wi
-  const int h = lane >> 5;
-
-  // source descriptors of this job's A columns and X columns
-  const int a_col0 = to * 128;
-  const int a_cols = min(128, pr.a_valid - a_col0);
-  const int x_col0 = ti * 128;
-  const E* xsrc;
-  int ldx, x_cols;
-  if (x_col0 < pr.x0_cols) {
-    xsrc = (const E*)pr.X0 + x_col0; ldx = pr.ldx0; x_cols = min(128, pr.x0_cols - x_col0);
-  } else {
-    xsrc = (const E*)pr.X1 + (x_col0 - pr.x0_cols); ldx = pr.ldx1;
-    x_cols = min(128, pr.in_valid - x_col0);
-  }
-  const E* asrc = (const E*)pr.A + a_col0;
-  const bool wave_live = (64 * wo < a_cols) && (64 * wi < x_cols);
-
-  f32x16 acc[2][2];
+    f32x16 acc[2][5];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
-  float dbacc[2] = {0.f, 0.f};
+      for (int j = 0; j < 5; ++j) acc[i][j] = f32x16{};
+    float dbacc[2] = {0.f, 0.f};
+    float sg = 0.f, sgb = 0.f;                   // sigma head: ds x y (feature tid & 255), sum ds
 
-  u32x4 ra[C::kPieces], rx[C::kPieces];
-  auto gload = [&](int mb) {
+    const char* pa0 = (const char*)pr.A;
+    const char* p00 = (const char*)pr.X0;
+    const char* p10 = pr.X1 ? (const char*)pr.X1 : p00;
+    auto src_of = [&](int tile, int b) -> const char* {
+      // byte b of the slab of wave tile `tile`: [A tiles | X0 tiles | X1 tiles]
+      if (b < a_bytes) return pa0 + (size_t)tile * pr.a_width * 32 * ES + b;
+      if (b < a_bytes + x0_bytes) return p00 + (size_t)tile * pr.x0_width * 32 * ES + (b - a_bytes);
+      if (b < a_bytes + x0_bytes + x1_bytes)
+        return p10 + (size_t)tile * pr.x1_width * 32 * ES + (b - a_bytes - x0_bytes);
+      return pa0;                                         // dummy piece
+    };
+    // bf16 staging: LDS-DMA ring, kDepth slabs in flight; every wave issues
+    // exactly kG 1-KiB pieces per slab (pieces past the slab re-read the
+    // first KiB into a dummy area) so one compile-time vmcnt fits all problems.
+    // The DMA is opaque to the compiler (glds16_opaque): the explicit vmcnt
+    // waits below are the only synchronisation.  The slab loop is unrolled by
+    // the ring size so every slot offset is a compile-time constant.
+    auto issue_dma = [&](int st, auto slotc) {
+      char* dst = smem + decltype(slotc)::value * kRingStage;
 #pragma unroll
-    for (int k = 0; k < C::kPieces; ++k) {
-      const int piece = threadIdx.x + 256 * k;
-      const int row = piece / kPPR, cp = piece % kPPR;
-      const int mm = mb + row;
-      const bool rok = mm < m1;
-      ra[k] = (rok && cp * kEPP < a_cols) ? *(const u32x4*)(asrc + (size_t)mm * pr.lda + cp * kEPP) : u32x4{};
-      rx[k] = (rok && cp * kEPP < x_cols) ? *(const u32x4*)(xsrc + (size_t)mm * ldx + cp * kEPP) : u32x4{};
+      for (int k = 0; k < kG; ++k) {
+        const int piece = w * kG + k;
+        glds16_opaque(src_of(slab(st), piece * 1024) + lane * 16, lds_addr(dst + piece * 1024));
+      }
+    };
+    // fp32 staging (parity path): registers, double buffered
+    u32x4 rg[C::kLoads];
+    auto gload = [&](int tile) {
+#pragma unroll
+      for (int k = 0; k < C::kLoads; ++k) {
+        const int b = (threadIdx.x + 512 * k) << 4;
+        rg[k] = (threadIdx.x + 512 * k) < stage_pieces ? *(const u32x4*)src_of(tile, b) : u32x4{};
+      }
+    };
+    auto lstore = [&](int buf) {
+      char* dst = smem + buf * kStage;
+#pragma unroll
+      for (int k = 0; k < C::kLoads; ++k)
+        if ((threadIdx.x + 512 * k) < stage_pieces) *(u32x4*)(dst + ((threadIdx.x + 512 * k) << 4)) = rg[k];
+    };
+
+    if constexpr (kBf16) {
+      static_for<0, kDepth>([&](auto i) {
+        if (i < nst) issue_dma(i, i);
+      });
+    } else {
+      if (nst > 0) {
+        gload(slab(0));
+        lstore(0);
+      }
+      __syncthreads();
     }
-  };
-  auto lstore = [&](int buf) {
-    char* A = smem + buf * 2 * kTile;
-    char* X = A + kTile;
-#pragma unroll
-    for (int k = 0; k < C::kPieces; ++k) {
-      const int piece = threadIdx.x + 256 * k;
-      const int row = piece / kPPR, cp = piece % kPPR;
-      *(u32x4*)(A + row * C::kRow + cp * 16) = ra[k];
-      *(u32x4*)(X + row * C::kRow + cp * 16) = rx[k];
-    }
-  };
-
-  const int nsteps = (m1 - m0 + 31) / 32;
-  if (nsteps > 0) {
-    gload(m0);
-    lstore(0);
-  }
-  __syncthreads();
-  for (int st = 0; st < nsteps; ++st) {
-    const int buf = st & 1;
-    if (st + 1 < nsteps) gload(m0 + 32 * (st + 1));
-    const char* A = smem + buf * 2 * kTile;
-    const char* X = A + kTile;
-    if (wave_live) {
+    constexpr int kRing = kBf16 ? kDepth + 1 : 2;
+    auto body = [&](int st, auto slotc) {
+      constexpr int SL = decltype(slotc)::value;
+      const char* A;
       if constexpr (kBf16) {
-        const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+        // slab st landed (own pieces), then every wave's pieces (barrier);
+        // the slot refilled below held slab st-1, which all waves finished.
+        const int ahead = min(kDepth - 1, nst - 1 - st);   // later slabs already issued
+        static_for<0, kDepth>([&](auto n) {
+          if (n == ahead) wait_vmcnt<n * kG>();
+        });
+        block_barrier();
+        if (st + kDepth < nst) issue_dma(st + kDepth, std::integral_constant<int, (SL + kDepth) % kRing>{});
+        A = smem + SL * kRingStage;
+      } else {
+        if (st + 1 < nst) gload(slab(st + 1));
+        A = smem + SL * kStage;
+      }
+      const char* X = A + a_bytes;
+      if (live) {
+        if constexpr (kBf16) {
+          const int G = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
 #pragma unroll
-        for (int kk = 0; kk < 32; kk += 16) {
-          bf16x8 fa[2], fx[2];
+          for (int kk = 0; kk < 32; kk += 16) {
+            const int s = kk + 8 * h + q;
+            bf16x8 fa[2];
 #pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            const int col = 64 * wo + 32 * i + 16 * (g & 1) + 4 * p;
-            const int row = kk + 8 * h + q;
-            const char* base = A + row * C::kRow + col * 2;
-            s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)base);
-            s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (__attribute__((address_space(3))) s16x4*)(base + 4 * C::kRow));
-            fa[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-            const int colx = 64 * wi + 32 * i + 16 * (g & 1) + 4 * p;
-            const char* bx = X + row * C::kRow + colx * 2;
-            s16x4 xl = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)bx);
-            s16x4 xh = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (__attribute__((address_space(3))) s16x4*)(bx + 4 * C::kRow));
-            fx[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(xl, xh, 0, 1, 2, 3, 4, 5, 6, 7));
+            for (int i = 0; i < 2; ++i) {
+              const int f = 64 * wo + 32 * i + 16 * (G & 1) + 4 * p;
+              s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(A + img_off<ES>(s, f)));
+              s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(A + img_off<ES>(s + 4, f)));
+              fa[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+              float sum = 0.f;
+#pragma unroll
+              for (int j = 0; j < 8; ++j) sum += (float)fa[i][j];
+              dbacc[i] += sum;
+            }
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+              if (j < 4 ? !cols_live : !extra) continue;
+              const int f = (j < 4 ? 128 * wi + 32 * j : 256) + 16 * (G & 1) + 4 * p;
+              s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(X + img_off<ES>(s, f)));
+              s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(X + img_off<ES>(s + 4, f)));
+              const bf16x8 fx = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+              acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fx, acc[0][j], 0, 0, 0);
+              if (row1_live) acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fx, acc[1][j], 0, 0, 0);
+            }
           }
+        } else {
+          const int c = lane & 31;
+#pragma unroll 4
+          for (int q = 0; q < 16; ++q) {
+            const int s = 2 * q + h;
+            float fa[2];
 #pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            float s = 0.f;
+            for (int i = 0; i < 2; ++i) {
+              const int f = 64 * wo + 32 * i + c;
+              fa[i] = *(const float*)(A + img_off<ES>(s, f & ~3) + (f & 3) * 4);
+              dbacc[i] += fa[i];
+            }
 #pragma unroll
-            for (int j = 0; j < 8; ++j) s += (float)fa[i][j];
-            dbacc[i] += s;
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fx[j], acc[i][j], 0, 0, 0);
+            for (int j = 0; j < 5; ++j) {
+              if (j < 4 ? !cols_live : !extra) continue;
+              const int f = (j < 4 ? 128 * wi + 32 * j : 256) + c;
+              const float fx = *(const float*)(X + img_off<ES>(s, f & ~3) + (f & 3) * 4);
+              acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[0], fx, acc[0][j], 0, 0, 0);
+              if (row1_live) acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[1], fx, acc[1][j], 0, 0, 0);
+            }
           }
         }
-      } else {
-        const int c = lane & 31;
+      }
+      if (pr.sigma_head) {
+        // d w_sigma[f] += sum_s ds[s] * y[s][f];  ds = A[s][256] + A[s][257]
+        const int f = threadIdx.x & 255;
+        const int s0 = (threadIdx.x >> 8) * 16;
+#pragma unroll 4
+        for (int s = s0; s < s0 + 16; ++s) {
+          const E* dsp = (const E*)(A + img_off<ES>(s, 256));
+          const float ds = (float)dsp[0] + (float)dsp[1];
+          const float y = (float)((const E*)(X + img_off<ES>(s, f & ~3)))[f & 3];
+          sg = __builtin_fmaf(ds, y, sg);
+          sgb += ds;
+        }
+      }
+      if constexpr (!kBf16) {
+        if (st + 1 < nst) lstore((st + 1) & 1);
+        __syncthreads();
+      }
+    };
+    for (int base = 0; base < nst; base += kRing)
+      static_for<0, kRing>([&](auto k) {
+        if (base + k < nst) body(base + k, k);
+      });
+    __syncthreads();
+
+    // ---- fp32 partial: row n (out feature), column c (in feature)
+    if (live) {
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const int row = 2 * q + h;
-          float fa[2], fx[2];
+      for (int i = 0; i < 2; ++i) {
+        if (i == 1 && !row1_live) continue;
 #pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            fa[i] = *(const float*)(A + row * C::kRow + (64 * wo + 32 * i + c) * 4);
-            fx[i] = *(const float*)(X + row * C::kRow + (64 * wi + 32 * i + c) * 4);
-          }
+        for (int j = 0; j < 5; ++j) {
+          if (j < 4 ? !cols_live : !extra) continue;
+          const int col = (j < 4 ? 128 * wi + 32 * j : 256) + (lane & 31);
 #pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            dbacc[i] += fa[i];
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i], fx[j], acc[i][j], 0, 0, 0);
+          for (int r = 0; r < 16; ++r) {
+            const int row = 64 * wo + 32 * i + acc_row(r, h);
+            part[(size_t)row * kPartCols + col] = acc[i][j][r];
           }
         }
       }
     }
-    if (st + 1 < nsteps) lstore(buf ^ 1);
+    if (wi == 0) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const float tot = dbacc[i] + __shfl_xor(dbacc[i], 32);
+        const bool rl = i == 0 ? row0_live : row1_live;
+        if (h == 0 && rl) dbpart[64 * wo + 32 * i + (lane & 31)] = tot;
+      }
+    }
+    if (pr.sigma_head) {
+      // combine the two sample halves through LDS (the staging buffers are free now)
+      float* red = (float*)smem;
+      red[threadIdx.x] = sg;
+      red[512 + threadIdx.x] = sgb;
+      __syncthreads();
+      if (threadIdx.x < 256) {
+        part[(size_t)256 * kPartCols + threadIdx.x] = red[threadIdx.x] + red[threadIdx.x + 256];
+        if (threadIdx.x == 0) dbpart[256] = red[512] + red[512 + 256];
+      }
+    }
     __syncthreads();
   }
+};
 
-  // ---- write the fp32 partial tile: row n (out feature), column c (in feature)
-  const int ldp = pr.in_tiles * 128;
-  float* part = pr.part + ((size_t)slice * pr.out_tiles * 128) * ldp;
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int col = ti * 128 + 64 * wi + 32 * j + (lane & 31);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = to * 128 + 64 * wo + 32 * i + acc_row(r, h);
-        part[(size_t)row * ldp + col] = acc[i][j][r];
-      }
-    }
-  if (wi == 0) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const float tot = dbacc[i] + __shfl_xor(dbacc[i], 32);
-      if (h == 0)
-        pr.dbpart[(size_t)slice * pr.out_tiles * 128 + to * 128 + 64 * wo + 32 * i + (lane & 31)] = tot;
-    }
+template <int P>
+__global__ __launch_bounds__(512, 2) void dw_kernel(DwArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[DwSeg<P>::kSmem];
+  const int g = blockIdx.x;
+  const long long total = a.wprefix[a.nprob];
+  const long long b0 = dw_share_begin(g, total, a.nwg), b1 = dw_share_begin(g + 1, total, a.nwg);
+  int seg = 0;
+  for (int p = 0; p < a.nprob && seg < 2; ++p) {
+    int t0, t1;
+    dw_slab_range(a.wprefix, a.pbytes, a.total_tiles, p, b0, b1, t0, t1);
+    if (t1 <= t0) continue;
+    const size_t slot = (size_t)g * 2 + seg;
+    DwSeg<P>::run(a.p[p], t0, t1, g * 613, a.part + slot * kPartRows * kPartCols, a.dbpart + slot * kPartRows, smem);
+    ++seg;
   }
 }
 
-__device__ __forceinline__ int pe_feature(int slot) { return pe_slot_feature(slot >> 5, slot & 31); }
-__device__ __forceinline__ int dir_feature(int slot) { return dir_slot_feature(slot >> 4, slot & 15); }
+// ---------------------------------------------------------------- reduction
+__device__ __forceinline__ int pe_feature(int c) { return pe_slot_feature(col_half(c), col_slot(c)); }
+__device__ __forceinline__ int dir_feature(int c) { return dir_slot_feature(col_half(c), col_slot(c)); }
 
 __global__ __launch_bounds__(256) void dw_reduce_kernel(DwRedArgs a) {
   const int gid = blockIdx.x * 256 + threadIdx.x;
@@ -213,27 +304,43 @@ __global__ __launch_bounds__(256) void dw_reduce_kernel(DwRedArgs a) {
   const DwRedProblem& p = a.p[pi];
   const int e = gid - a.prefix[pi];
   const int n = e / p.cols, c = e % p.cols;
-  const size_t slice_stride = (size_t)p.rows_pad * p.ldp;
-  float v = 0.f;
-  for (int s = 0; s < a.slices; ++s) v += p.part[s * slice_stride + (size_t)n * p.ldp + c];
-  float db = 0.f;
+  // workgroups whose share holds slabs of problem pi (contiguous range)
+  const long long total = a.wprefix[a.nprob];
+  int g_lo = (int)(a.wprefix[pi] * a.nwg / (total > 0 ? total : 1)) - 1;
+  int g_hi = (int)(a.wprefix[pi + 1] * a.nwg / (total > 0 ? total : 1)) + 1;
+  g_lo = max(0, g_lo);
+  g_hi = min(a.nwg - 1, g_hi);
+  float v = 0.f, db = 0.f;
   const bool need_db = (c == 0) || p.z;
-  if (need_db)
-    for (int s = 0; s < a.slices; ++s) db += p.dbpart[(size_t)s * p.rows_pad + n];
-  if (p.z && n < p.out_real && c < p.in_real) v += db * p.z[c];
-  // destination
-  if (p.map == MAP_VIEWDIR && n >= p.out_real) {          // sigma-head rows (value, residual)
-    if (n == p.out_real) {
-      // combine both rows here so the accumulation into .grad stays race-free
-      float v2 = 0.f, db2 = 0.f;
-      for (int s = 0; s < a.slices; ++s) v2 += p.part[s * slice_stride + (size_t)(n + 1) * p.ldp + c];
-      if (c == 0)
-        for (int s = 0; s < a.slices; ++s) db2 += p.dbpart[(size_t)s * p.rows_pad + n + 1];
-      if (c < 256) a.grads[p.w2][c] += v + v2;
-      if (c == 0) a.grads[p.b2][0] += db + db2;
+  for (int g = g_lo; g <= g_hi; ++g) {
+    const long long b0 = dw_share_begin(g, total, a.nwg), b1 = dw_share_begin(g + 1, total, a.nwg);
+    // does g own slabs of pi?  (start byte of pi's slab t is wprefix + t*pb)
+    const long long lo = max(b0, a.wprefix[pi]), hi = min(b1, a.wprefix[pi + 1]);
+    if (hi <= lo) continue;
+    // a slab start inside [lo, hi)?
+    const long long pb = p.pbytes;
+    const long long first = ((lo - a.wprefix[pi]) + pb - 1) / pb * pb + a.wprefix[pi];
+    if (first >= hi) continue;
+    // segment index: 1 if the previous problem also has slabs in g
+    int seg = 0;
+    if (pi > 0) {
+      const long long lo2 = max(b0, a.wprefix[pi - 1]), hi2 = min(b1, a.wprefix[pi]);
+      if (hi2 > lo2) {
+        const long long pb2 = a.p[pi - 1].pbytes;
+        const long long f2 = ((lo2 - a.wprefix[pi - 1]) + pb2 - 1) / pb2 * pb2 + a.wprefix[pi - 1];
+        if (f2 < hi2) seg = 1;
+      }
     }
+    const size_t slot = (size_t)g * 2 + seg;
+    v += a.part[slot * kPartRows * kPartCols + (size_t)n * kPartCols + c];
+    if (need_db) db += a.dbpart[slot * kPartRows + n];
+  }
+  if (p.map == MAP_VIEWDIR && n == p.out_real) {          // sigma-head row
+    if (c < 256) a.grads[p.w2][c] += v;
+    if (c == 0) a.grads[p.b2][0] += db;
     return;
   }
+  if (p.z && n < p.out_real && c < p.in_real) v += db * p.z[c];
   if (n >= p.out_real) return;
   int f = c;
   if (p.map == MAP_PE) f = pe_feature(c);

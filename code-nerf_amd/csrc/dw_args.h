@@ -6,51 +6,78 @@ namespace cn {
 
 constexpr int kDwMaxProblems = 12;
 
+// One layer's weight gradient over one slice of the samples.  Operands are
+// wave-tiled planes (cn_layout.h): a 32-sample slab of T feature tiles is one
+// contiguous run of T * 1024 elements.
 struct DwProblem {
-  const void* A;        // [Mp][lda] gradient plane (out features)
-  int lda, a_valid;     // plane width, valid out features
-  const void* X0;       // [Mp][ldx0] input plane for columns [0, x0_cols)
-  int ldx0, x0_cols;
-  const void* X1;       // [Mp][ldx1] input plane for columns [x0_cols, in_valid)
-  int ldx1, in_valid;
-  int out_tiles, in_tiles;
-  float* part;          // [S][out_tiles*128][in_tiles*128]
-  float* dbpart;        // [S][out_tiles*128]
+  const void* A;        // gradient plane (rows of dW: out features)
+  int a_width;          // plane width (elements)
+  int a_tiles;          // 32-wide feature tiles of A staged per slab (<= 9)
+  int out_tiles;        // row tiles computed by MFMA (<= 8)
+  const void* X0;       // input plane, feature tiles [0, x0_tiles)
+  int x0_width, x0_tiles;
+  const void* X1;       // second input plane appended after X0 (dir PE), or null
+  int x1_width, x1_tiles;
+  int sigma_head;       // viewdir: also sum ds (A column 256 + 257) x X columns 0..255
+  int rows_pad, cols_pad;   // extent of the partial actually written (<= 288)
 };
 
+// Persistent, byte-balanced schedule: the (problem, slab) stream -- problem
+// after problem, slab after slab -- is cut into `nwg` equal shares of HBM
+// bytes; workgroup g owns share g and so at most two consecutive problems
+// ("segments"); it writes one partial per segment into slot (g, seg).
 struct DwArgs {
   DwProblem p[kDwMaxProblems];
   int nprob;
-  int M;
-  int slices;
-  int mchunk;           // samples per slice (multiple of 32)
-  int tile_prefix[kDwMaxProblems + 1];   // cumulative out_tiles*in_tiles
+  int total_tiles;              // slabs per problem (Mp / 32)
+  int nwg;                      // workgroups (= partial slots / 2)
+  long long wprefix[kDwMaxProblems + 1];   // cumulative bytes: problem p starts at wprefix[p]
+  int pbytes[kDwMaxProblems];   // bytes per slab of problem p
+  float* part;                  // [nwg][2][kPartRows][kPartCols]
+  float* dbpart;                // [nwg][2][kPartRows]
 };
+constexpr int kPartRows = 288, kPartCols = 288;
+
+#define CN_HD __host__ __device__ __forceinline__
+// first byte of workgroup g's share
+CN_HD long long dw_share_begin(int g, long long total, int nwg) { return total * g / nwg; }
+// slabs [t0, t1) of problem p whose first byte lies in [b0, b1)
+CN_HD void dw_slab_range(const long long* wprefix, const int* pbytes, int T, int p, long long b0, long long b1,
+                         int& t0, int& t1) {
+  const long long base = wprefix[p], pb = pbytes[p];
+  auto cdiv = [&](long long x) -> int {
+    if (x <= 0) return 0;
+    const long long q = (x + pb - 1) / pb;
+    return q > T ? T : (int)q;
+  };
+  t0 = cdiv(b0 - base);
+  t1 = cdiv(b1 - base);
+}
 
 enum DwMap : int { MAP_PLAIN = 0, MAP_PE = 1, MAP_VIEWDIR = 2 };
 
 struct DwRedProblem {
-  const float* part;
-  const float* dbpart;
-  int ldp;              // in_tiles*128
-  int rows_pad;         // out_tiles*128 (dbpart stride per slice)
   int out_real;         // rows mapped to the weight tensor
   int in_real;          // reference input width of the weight tensor
-  int cols;             // columns to visit (in_valid)
+  int cols;             // columns to visit
   int map;              // DwMap
   int w, b;             // weight / bias tensor indices
-  int w2, b2;           // viewdir: sigma-head weight / bias tensor indices
+  int w2, b2;           // viewdir: sigma-head weight / bias tensor indices (row out_real)
   const float* z;       // injection vector of the layer input (or null)
   float* dbout;         // this call's bias gradient (for the latent backward) or null
-  int elems;            // work items: (out_real + extra rows) * cols
+  int elems;            // work items
+  int pbytes;           // bytes per slab (schedule)
 };
 
 struct DwRedArgs {
   DwRedProblem p[kDwMaxProblems];
   int nprob;
-  int slices;
   int prefix[kDwMaxProblems + 1];
   float* const* grads;
+  int nwg;
+  long long wprefix[kDwMaxProblems + 1];
+  const float* part;            // DwArgs::part
+  const float* dbpart;
 };
 
 }  // namespace cn

@@ -112,9 +112,11 @@ CN_DEV void ray_forward(RayState& st, const float* sig, const float* rgb, const 
       st.e[k] = expf(-fmul_rn(st.sig[k], st.delta[k]));
       st.alpha[k] = 1.f - st.e[k];
       st.trans[k] = fadd_rn(1.f - st.alpha[k], 1e-10f);
-      st.c[k][0] = rgb[3 * s + 0];
-      st.c[k][1] = rgb[3 * s + 1];
-      st.c[k][2] = rgb[3 * s + 2];
+      if (rgb) {
+        st.c[k][0] = rgb[3 * s + 0];
+        st.c[k][1] = rgb[3 * s + 1];
+        st.c[k][2] = rgb[3 * s + 2];
+      }
       prod *= (double)st.trans[k];
     }
   }
@@ -269,6 +271,174 @@ __global__ __launch_bounds__(256) void chunk_loss_kernel(const float* __restrict
     __syncthreads();
   }
   if (threadIdx.x == 0) loss[c] = (float)(red[0] / (3.0 * (b - a)));
+}
+
+// ---------------------------------------------------------------- fine pass
+// Hierarchical ("coarse + fine") sampling: the BASELINE configs' 64 + 64
+// samples.  The reference has no fine pass, so this
+// follows NeRF's sample_pdf with the CodeNeRF MLP shared by both passes;
+// oracle: oracle/ref_cpu.py sample_pdf / fine_render_loss (parity unpinned).
+
+// Importance samples of one ray per wave: bins = midpoints of the coarse z,
+// pdf = (w[1:-1] + 1e-5) / sum, cdf = [0, cumsum] (float64, rounded once),
+// u_j = (j + rnd_j) / Nf (stratified, so z_f comes out sorted), z_f = inverse
+// cdf with NeRF's degenerate-bin rule (denom < 1e-5 -> 1).
+constexpr int kMaxRaySamples = 64 * kMaxPer;
+
+__global__ __launch_bounds__(256) void sample_pdf_kernel(const float* __restrict__ sig, const float* __restrict__ z,
+                                                         int z_stride, int R, int Nc,
+                                                         const float* __restrict__ rnd, int Nf,
+                                                         float* __restrict__ zf) {
+  __shared__ float cdf_s[4][kMaxRaySamples], bin_s[4][kMaxRaySamples];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + wv;
+  if (r >= R) return;                       // wave-uniform; no block barriers below
+  const float* zr = z + (size_t)r * z_stride;
+  RayState st;
+  ray_forward(st, sig + (size_t)r * Nc, nullptr, zr, Nc);
+  // interior weights s = 1 .. Nc-2, +1e-5 (float, as torch: weights + 1e-5)
+  float wv_[kMaxPer];
+  double part = 0.0;
+#pragma unroll
+  for (int k = 0; k < kMaxPer; ++k) {
+    const int s = st.n0 + k;
+    wv_[k] = 0.f;
+    if (k < st.cnt && s >= 1 && s <= Nc - 2) {
+      wv_[k] = st.w[k] + 1e-5f;
+      part += (double)wv_[k];
+    }
+  }
+  // exclusive prefix over lanes
+  double incl = part;
+#pragma unroll
+  for (int k = 1; k < 64; k <<= 1) {
+    const double o = shfl_up_d(incl, k);
+    if (lane >= k) incl += o;
+  }
+  double total = incl;
+  total = __hiloint2double(__shfl(__double2hiint(total), 63), __shfl(__double2loint(total), 63));
+  double run = incl - part;
+  float* cdf = cdf_s[wv];
+  float* bins = bin_s[wv];
+#pragma unroll
+  for (int k = 0; k < kMaxPer; ++k) {
+    const int s = st.n0 + k;
+    if (k < st.cnt) {
+      run += (double)wv_[k];
+      // cdf[i] = sum_{s=1..i} / total for i = 1 .. Nc-2; cdf[0] = 0
+      if (s >= 1 && s <= Nc - 2) cdf[s] = (float)(run / total);
+      if (s == 0) cdf[0] = 0.f;
+      if (s + 1 < Nc) bins[s] = fmul_rn(0.5f, fadd_rn(zr[s], zr[s + 1]));
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int nb = Nc - 1;                    // cdf / bin entries
+  for (int j = lane; j < Nf; j += 64) {
+    const float u = (float)j + rnd[(size_t)r * Nf + j];
+    const float uu = u / (float)Nf;
+    // searchsorted(cdf, uu, right=True): first index with cdf > uu
+    int lo = 0, hi = nb;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (cdf[mid] <= uu) lo = mid + 1; else hi = mid;
+    }
+    const int below = max(0, lo - 1), above = min(nb - 1, lo);
+    const float cb = cdf[below], ca = cdf[above];
+    const float bb = bins[below], ba = bins[above];
+    float denom = fadd_rn(ca, -cb);
+    if (denom < 1e-5f) denom = 1.f;
+    const float t = fadd_rn(uu, -cb) / denom;
+    zf[(size_t)r * Nf + j] = fadd_rn(bb, fmul_rn(t, fadd_rn(ba, -bb)));
+  }
+}
+
+// Fine composite + chunk-mean MSE + backward over the union of the coarse
+// and fine samples of each ray (merged by z; a coarse sample precedes a fine
+// one at equal z).  dsig_c / drgb_c are ACCUMULATED into (they already hold
+// the coarse loss's gradient); dsig_f / drgb_f are written.
+__global__ __launch_bounds__(256) void fine_render_loss_kernel(
+    const float* __restrict__ sig_c, const float* __restrict__ rgb_c, const float* __restrict__ zc, int zc_stride,
+    int Nc, const float* __restrict__ sig_f, const float* __restrict__ rgb_f, const float* __restrict__ zf, int Nf,
+    int R, int white_bg, const float* __restrict__ gt, int chunk, float* __restrict__ out_rgb,
+    float* __restrict__ ray_se, float* __restrict__ dsig_c, float* __restrict__ drgb_c,
+    float* __restrict__ dsig_f, float* __restrict__ drgb_f) {
+  __shared__ float m_sig[4][kMaxRaySamples], m_z[4][kMaxRaySamples], m_rgb[4][kMaxRaySamples * 3];
+  __shared__ float m_dsig[4][kMaxRaySamples], m_drgb[4][kMaxRaySamples * 3];
+  __shared__ int m_src[4][kMaxRaySamples];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + wv;
+  if (r >= R) return;                       // wave-uniform; only wave-level sync below
+  const int N = Nc + Nf;
+  const float* zcr = zc + (size_t)r * zc_stride;
+  const float* zfr = zf + (size_t)r * Nf;
+  auto wave_sync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  // merged position = own index + number of the other list's samples before it
+  for (int i = lane; i < Nc; i += 64) {
+    const float v = zcr[i];
+    int lo = 0, hi = Nf;                    // count zf < v
+    while (lo < hi) { const int mid = (lo + hi) >> 1; if (zfr[mid] < v) lo = mid + 1; else hi = mid; }
+    const int p = i + lo;
+    const size_t g = (size_t)r * Nc + i;
+    m_sig[wv][p] = sig_c[g];
+    m_z[wv][p] = v;
+    m_rgb[wv][3 * p + 0] = rgb_c[3 * g + 0];
+    m_rgb[wv][3 * p + 1] = rgb_c[3 * g + 1];
+    m_rgb[wv][3 * p + 2] = rgb_c[3 * g + 2];
+    m_src[wv][p] = i;
+  }
+  for (int j = lane; j < Nf; j += 64) {
+    const float v = zfr[j];
+    int lo = 0, hi = Nc;                    // count zc <= v
+    while (lo < hi) { const int mid = (lo + hi) >> 1; if (zcr[mid] <= v) lo = mid + 1; else hi = mid; }
+    const int p = j + lo;
+    const size_t g = (size_t)r * Nf + j;
+    m_sig[wv][p] = sig_f[g];
+    m_z[wv][p] = v;
+    m_rgb[wv][3 * p + 0] = rgb_f[3 * g + 0];
+    m_rgb[wv][3 * p + 1] = rgb_f[3 * g + 1];
+    m_rgb[wv][3 * p + 2] = rgb_f[3 * g + 2];
+    m_src[wv][p] = Nc + j;
+  }
+  wave_sync();
+  RayState st;
+  ray_forward(st, m_sig[wv], m_rgb[wv], m_z[wv], N);
+  float o[5];
+  ray_reduce(st, o);
+  float col[3], gr[3];
+  const int c0 = (r / chunk) * chunk;
+  const int nbr = min(chunk, R - c0);
+  const float inv = 1.f / (float)(3 * nbr);
+  float se = 0.f;
+  for (int c = 0; c < 3; ++c) {
+    col[c] = white_bg ? fadd_rn(o[c] + 1.f, -o[4]) : o[c];
+    const float diff = col[c] - gt[3 * r + c];
+    se += diff * diff;
+    gr[c] = fmul_rn(fmul_rn(inv, 2.f), diff);
+  }
+  if (lane == 0) {
+    for (int c = 0; c < 3; ++c) out_rgb[3 * r + c] = col[c];
+    ray_se[r] = se;
+  }
+  ray_backward(st, gr, 0.f, white_bg, m_dsig[wv], m_drgb[wv]);
+  wave_sync();
+  for (int p = lane; p < N; p += 64) {
+    const int src = m_src[wv][p];
+    if (src < Nc) {
+      const size_t g = (size_t)r * Nc + src;
+      dsig_c[g] += m_dsig[wv][p];
+      for (int c = 0; c < 3; ++c) drgb_c[3 * g + c] += m_drgb[wv][3 * p + c];
+    } else {
+      const size_t g = (size_t)r * Nf + (src - Nc);
+      dsig_f[g] = m_dsig[wv][p];
+      for (int c = 0; c < 3; ++c) drgb_f[3 * g + c] = m_drgb[wv][3 * p + c];
+    }
+  }
 }
 
 // ---------------------------------------------------------------- misc

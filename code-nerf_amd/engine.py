@@ -96,13 +96,18 @@ class Engine:
 
     # ------------------------------------------------------------ MLP
     def mlp_fwd(self, blob, M, xyz=None, viewdir=None, rays_o=None, rays_d=None, z=None, z_stride=0,
-                n_samples=0, act=None):
+                n_samples=0, act=None, act_M=0, act_row0=0, sigma=None, rgb=None):
+        """act_M / act_row0: the workspace is sized for act_M samples and this
+        pass fills rows [act_row0, act_row0 + pad(M)) (coarse + fine passes)."""
         Mp = self.pad(M)
-        sigma = torch.empty(Mp, dtype=torch.float32, device=self.device)
-        rgb = torch.empty(Mp, 3, dtype=torch.float32, device=self.device)
+        if sigma is None:
+            sigma = torch.empty(Mp, dtype=torch.float32, device=self.device)
+        if rgb is None:
+            rgb = torch.empty(Mp, 3, dtype=torch.float32, device=self.device)
+        assert sigma.numel() >= Mp and rgb.numel() >= 3 * Mp
         check(self.L.cn_mlp_fwd(self._plan, ptr(self.pack_fwd), ptr(blob), M, ptr(xyz), ptr(viewdir),
                                 ptr(rays_o), ptr(rays_d), ptr(z), z_stride, n_samples, ptr(sigma), ptr(rgb),
-                                ptr(act), self.stream), "cn_mlp_fwd")
+                                ptr(act), int(act_M), int(act_row0), self.stream), "cn_mlp_fwd")
         return sigma, rgb
 
     def new_act(self, M):
@@ -167,6 +172,34 @@ def render_loss(sigma, rgb, z, R, N, gt, chunk, white_bg=True, dsig=None, drgb=N
                            ptr(out_rgb), ptr(ray_se), ptr(chunk_loss), ptr(dsig), ptr(drgb), _dev_stream(sigma)),
           "cn_render_loss")
     return out_rgb, chunk_loss, dsig, drgb
+
+
+def sample_pdf(sigma_c, z_c, R, Nc, rand):
+    """Fine z (R, Nf) from the coarse densities; rand (R, Nf) in [0, 1)."""
+    L = _lib.lib()
+    Nf = rand.shape[-1]
+    zc_stride = 0 if z_c.numel() == Nc else Nc
+    z_f = torch.empty(R, Nf, dtype=torch.float32, device=sigma_c.device)
+    check(L.cn_sample_pdf(ptr(sigma_c), ptr(z_c), zc_stride, R, Nc, ptr(rand), Nf, ptr(z_f),
+                          _dev_stream(sigma_c)), "cn_sample_pdf")
+    return z_f
+
+
+def render_loss_fine(sigma_c, rgb_c, z_c, Nc, sigma_f, rgb_f, z_f, Nf, R, gt, chunk, dsig_c, drgb_c,
+                     dsig_f, drgb_f, white_bg=True):
+    """Fine composite + MSE over the merged samples; accumulates into
+    dsig_c / drgb_c, writes dsig_f / drgb_f.  -> (rgb (R,3), chunk losses)."""
+    L = _lib.lib()
+    dev = sigma_c.device
+    zc_stride = 0 if z_c.numel() == Nc else Nc
+    out_rgb = torch.empty(R, 3, dtype=torch.float32, device=dev)
+    ray_se = torch.empty(R, dtype=torch.float32, device=dev)
+    chunk_loss = torch.empty((R + chunk - 1) // chunk, dtype=torch.float32, device=dev)
+    check(L.cn_render_loss_fine(ptr(sigma_c), ptr(rgb_c), ptr(z_c), zc_stride, Nc, ptr(sigma_f), ptr(rgb_f),
+                                ptr(z_f), Nf, R, int(white_bg), ptr(gt), chunk, ptr(out_rgb), ptr(ray_se),
+                                ptr(chunk_loss), ptr(dsig_c), ptr(drgb_c), ptr(dsig_f), ptr(drgb_f),
+                                _dev_stream(sigma_c)), "cn_render_loss_fine")
+    return out_rgb, chunk_loss
 
 
 def get_rays_dev(H, W, focal, focal_is_f64, c2w):

@@ -80,6 +80,72 @@ class ImageStep:
                        texture_table.grad[obj_idx], self.reg_coef if reg else 0.0, reg_out)
         return chunk_loss, out_rgb, reg_out
 
+    def forward_backward_fine(self, rays_o, viewdirs, z_c, rand_f, gt, shape_table, texture_table, obj_idx,
+                              reg=True):
+        """Coarse + fine image step (the BASELINE configs' "64 + 64"; no
+        reference counterpart -- NeRF hierarchical sampling through the one
+        CodeNeRF MLP, oracle/ref_cpu.py:fine_image_step).  Loss = coarse
+        chunk-mean MSE + fine chunk-mean MSE (+ code regulariser once).  The
+        coarse pass fills activation rows [0, pad(R*Nc)), the fine pass the
+        rows after, so one backward and one dW cover both.
+        Returns (coarse chunk losses, fine chunk losses, fine rgb (R,3), reg)."""
+        model = self.model
+        eng = model.engine()
+        params = model.param_list()
+        grads = self.ensure_grads(params)
+        self.ensure_grads([shape_table, texture_table])
+        R = rays_o.shape[0]
+        Nc = z_c.shape[-1]
+        Nf = rand_f.shape[-1]
+        Mc, Mf = R * Nc, R * Nf
+        Mc_p = eng.pad(Mc)
+        M = Mc_p + Mf
+        Mp = eng.pad(M)
+        z_c = z_c.contiguous().to(eng.device, torch.float32)
+        buf = self._buffers(eng, M)
+        if "sig" not in buf:
+            buf.update(sig=torch.empty(Mp, dtype=torch.float32, device=eng.device),
+                       rgb=torch.empty(Mp, 3, dtype=torch.float32, device=eng.device),
+                       dsig=torch.empty(Mp, dtype=torch.float32, device=eng.device),
+                       drgb=torch.empty(Mp, 3, dtype=torch.float32, device=eng.device))
+        sig, rgb, dsig, drgb = buf["sig"], buf["rgb"], buf["dsig"], buf["drgb"]
+        dsig.zero_()
+        drgb.zero_()
+        eng.ensure_packed(params, bwd=True)
+        s, t = shape_table.detach()[obj_idx], texture_table.detach()[obj_idx]
+        blob, zvec = eng.latent_fwd(params, s, t)
+        tm = self.timers
+        ev = tm.mark("fwd") if tm else None
+        sig_c, rgb_c = eng.mlp_fwd(blob, Mc, rays_o=rays_o, rays_d=viewdirs, z=z_c,
+                                   z_stride=0 if z_c.dim() == 1 else Nc, n_samples=Nc, act=buf["act"], act_M=M,
+                                   act_row0=0, sigma=sig[:Mc_p], rgb=rgb[:Mc_p])
+        if tm:
+            tm.done("fwd", ev)
+        _, loss_c, _, _ = _eng.render_loss(sig_c, rgb_c, z_c, R, Nc, gt, self.chunk, self.white_bg,
+                                           dsig=dsig[:Mc], drgb=drgb[:Mc])
+        z_f = _eng.sample_pdf(sig_c, z_c, R, Nc, rand_f)
+        ev = tm.mark("fwd") if tm else None
+        sig_f, rgb_f = eng.mlp_fwd(blob, Mf, rays_o=rays_o, rays_d=viewdirs, z=z_f, z_stride=Nf, n_samples=Nf,
+                                   act=buf["act"], act_M=M, act_row0=Mc_p, sigma=sig[Mc_p:], rgb=rgb[Mc_p:])
+        if tm:
+            tm.done("fwd", ev)
+        out_f, loss_f = _eng.render_loss_fine(sig_c, rgb_c, z_c, Nc, sig_f, rgb_f, z_f, Nf, R, gt, self.chunk,
+                                              dsig[:Mc], drgb[:Mc], dsig[Mc_p:Mc_p + Mf],
+                                              drgb[Mc_p:Mc_p + Mf], self.white_bg)
+        ev = tm.mark("bwd") if tm else None
+        eng.mlp_bwd(blob, M, dsig, drgb, buf["act"])
+        if tm:
+            tm.done("bwd", ev)
+            ev = tm.mark("dw")
+        eng.mlp_dw(buf["act"], M, zvec, grads, buf["dbuf"], buf["dw"])
+        if tm:
+            tm.done("dw", ev)
+        reg_out = torch.zeros(1, dtype=torch.float32, device=eng.device)
+        eng.latent_bwd(params, grads, s, t, zvec, buf["dbuf"], shape_table.grad[obj_idx],
+                       texture_table.grad[obj_idx], self.reg_coef if reg else 0.0, reg_out)
+        self.last_z_f = z_f
+        return loss_c, loss_f, out_f, reg_out
+
     @torch.no_grad()
     def render(self, rays_o, viewdirs, z_vals, shape_code, texture_code):
         """Forward only (src/optimizer.py:108-124): -> rgb (R,3), depth (R,)."""

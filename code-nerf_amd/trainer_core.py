@@ -2,7 +2,8 @@
 
 Mirrors the per-object body of the reference loop (src/trainer.py:58-85):
 rays from the pose, stratified z, the fused image forward/backward
-(render.ImageStep), then AdamW over the model and both code tables
+(render.ImageStep; with n_fine > 0 the coarse + fine step, an extension the
+reference lacks), then AdamW over the model and both code tables
 (src/trainer.py:114-120).  Gradients live in one flat fp32 buffer (every
 ``.grad`` is a view into it), so zeroing is one memset and the data-parallel
 exchange is one RCCL all-reduce of 2.9 MB + the code tables per step.
@@ -17,13 +18,12 @@ from .render import ImageStep
 class TrainCore:
     def __init__(self, model, shape_codes, texture_codes, near, far, n_coarse, n_fine=0, chunk=2048,
                  reg_coef=1e-4, lr=(1e-4, 1e-3), timers=None, dist=None):
-        if n_fine:
-            raise NotImplementedError("fine sampling is added by TrainCoreFine")
         self.model = model
         self.shape_codes = shape_codes
         self.texture_codes = texture_codes
         self.near, self.far = float(near), float(far)
         self.n_coarse = int(n_coarse)
+        self.n_fine = int(n_fine)
         self.dist = dist
         self.step_impl = ImageStep(model, chunk=chunk, reg_coef=reg_coef, timers=timers)
         tensors = model.param_list() + [shape_codes, texture_codes]
@@ -49,8 +49,14 @@ class TrainCore:
         ro, vd = _eng.get_rays_dev(H, W, focal, True, c2w)
         z = self.stratified_z(dev)
         self.flat_grad.zero_()
-        losses, rgb, reg = self.step_impl.forward_backward(ro, vd, z, gt, self.shape_codes, self.texture_codes,
-                                                           obj)
+        if self.n_fine:
+            rand_f = torch.rand(H * W, self.n_fine, device=dev)
+            loss_c, loss_f, rgb, reg = self.step_impl.forward_backward_fine(
+                ro, vd, z, rand_f, gt, self.shape_codes, self.texture_codes, obj)
+            losses = (loss_c, loss_f)
+        else:
+            losses, rgb, reg = self.step_impl.forward_backward(ro, vd, z, gt, self.shape_codes,
+                                                               self.texture_codes, obj)
         if self.dist is not None:
             self.dist.all_reduce(self.flat_grad)
         self.opt.step()

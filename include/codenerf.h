@@ -72,11 +72,15 @@ int cn_latent_fwd(const cn_plan *plan, const float *const *d_params, const float
  *   (src/utils.py:30), z = d_z[ray * z_stride + s] (z_stride 0: one z vector
  *   shared by all rays as in the reference, n_samples: per-ray z).
  * d_sigma [Mp], d_rgb [Mp][3].  d_act != NULL stores what the backward
- * needs (cn_act_bytes(plan, M) bytes). */
+ * needs: the workspace holds cn_act_bytes(plan, act_M) bytes (act_M <= 0:
+ * act_M = M) and this call fills its sample rows [act_row0, act_row0 + Mp)
+ * (act_row0 a multiple of cn_pad_samples' granule, 256), so the coarse and
+ * the fine pass of one image share one workspace and one backward. */
 int cn_mlp_fwd(const cn_plan *plan, const void *d_pack_fwd, const float *d_blob, int M,
                const float *d_xyz, const float *d_viewdir, const float *d_rays_o,
                const float *d_rays_d, const float *d_z, int z_stride, int n_samples,
-               float *d_sigma, float *d_rgb, void *d_act, void *stream);
+               float *d_sigma, float *d_rgb, void *d_act, int act_M, int act_row0,
+               void *stream);
 
 /* ---- autograd of CodeNeRF.forward (src/trainer.py:82): dX chain. */
 int cn_mlp_bwd(const cn_plan *plan, const void *d_pack_bwd, const float *d_blob, int M,
@@ -119,6 +123,25 @@ int cn_render_loss(const float *d_sigma, const float *d_rgb, const float *d_z, i
                    int R, int N, int white_bg, const float *d_gt, int chunk, float *d_out_rgb,
                    float *d_ray_se, float *d_chunk_loss, float *d_dsigma, float *d_drgb,
                    void *stream);
+
+/* ---- hierarchical sampling (BASELINE configs' "64 coarse + 64 fine"; the
+ * reference has no fine pass -- NeRF's sample_pdf restated, oracle
+ * oracle/ref_cpu.py:sample_pdf).  Per ray: bins = midpoints of the coarse z,
+ * pdf = weights[1:-1] + 1e-5 normalised, u_j = (j + d_rand[ray][j]) / Nf,
+ * d_z_f [R][Nf] = inverse cdf (ascending). */
+int cn_sample_pdf(const float *d_sigma_c, const float *d_z_c, int zc_stride, int R, int Nc,
+                  const float *d_rand, int Nf, float *d_z_f, void *stream);
+
+/* fine composite over the union of each ray's coarse and fine samples
+ * (merged by z) + chunk-mean MSE + backward.  d_dsig_c / d_drgb_c are
+ * accumulated into (they hold the coarse loss's gradient from
+ * cn_render_loss); d_dsig_f / d_drgb_f [R*Nf] are written. */
+int cn_render_loss_fine(const float *d_sigma_c, const float *d_rgb_c, const float *d_z_c,
+                        int zc_stride, int Nc, const float *d_sigma_f, const float *d_rgb_f,
+                        const float *d_z_f, int Nf, int R, int white_bg, const float *d_gt,
+                        int chunk, float *d_out_rgb, float *d_ray_se, float *d_chunk_loss,
+                        float *d_dsig_c, float *d_drgb_c, float *d_dsig_f, float *d_drgb_f,
+                        void *stream);
 
 /* ---- torch.optim.AdamW step (src/trainer.py:116-120) over nseg tensors
  * (host arrays of device pointers), step = 1-based count of this update. */

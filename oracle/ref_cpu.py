@@ -174,6 +174,98 @@ def image_step(p, shape_table, texture_table, obj_idx, ro, vd, z_vals, gt, chunk
     return losses, torch.cat(outs)
 
 
+# ---------------------------------------------------------------- fine pass
+# The BASELINE configs' "64 coarse + 64 fine" has no counterpart in the
+# reference (one stratified pass only, src/utils.py:21-32; SURVEY.md section
+# 0): these restate NeRF's hierarchical sampling as the HIP path defines it
+# (include/codenerf.h cn_sample_pdf / cn_render_loss_fine).  PARITY UNPINNED:
+# no reference output exists; they check the HIP kernels' self-consistency.
+def composite_weights(sigmas, z_vals):
+    """The weights alpha * T of volume_rendering (src/utils.py:36-42)."""
+    sig = sigmas[..., 0] if sigmas.dim() == 3 else sigmas
+    gaps = z_vals[..., 1:] - z_vals[..., :-1]
+    gaps = torch.cat([gaps, torch.full_like(gaps[..., :1], 1e10)], -1)
+    alpha = 1 - torch.exp(-sig * gaps)
+    keep = 1 - alpha + 1e-10
+    T = torch.cumprod(torch.cat([torch.ones_like(keep[..., :1]), keep], -1), -1)[..., :-1]
+    return alpha * T
+
+
+def sample_pdf(sigmas, z_vals, rand):
+    """Importance samples (R, Nf): bins = coarse-z midpoints, pdf = w[1:-1] +
+    1e-5 normalised, cdf = [0, cumsum] (float64, rounded once), stratified
+    u_j = (j + rand_j) / Nf, inverse cdf with NeRF's degenerate-bin rule."""
+    R, Nc = sigmas.shape[0], sigmas.shape[-1] if sigmas.dim() == 2 else sigmas.shape[1]
+    sig = sigmas.reshape(R, Nc)
+    z = z_vals.expand(R, Nc) if z_vals.dim() == 1 else z_vals
+    w = composite_weights(sig, z)[:, 1:-1] + 1e-5
+    cs = torch.cumsum(w.double(), -1)
+    cdf = torch.cat([torch.zeros(R, 1, dtype=torch.float32), (cs / cs[:, -1:]).float()], -1)   # (R, Nc-1)
+    bins = 0.5 * (z[:, :-1] + z[:, 1:])
+    Nf = rand.shape[-1]
+    u = (torch.arange(Nf, dtype=torch.float32)[None, :] + rand) / Nf
+    inds = torch.searchsorted(cdf, u.contiguous(), right=True)
+    below = torch.clamp(inds - 1, min=0)
+    above = torch.clamp(inds, max=Nc - 2)
+    cb, ca = torch.gather(cdf, 1, below), torch.gather(cdf, 1, above)
+    bb, ba = torch.gather(bins, 1, below), torch.gather(bins, 1, above)
+    denom = ca - cb
+    denom = torch.where(denom < 1e-5, torch.ones_like(denom), denom)
+    t = (u - cb) / denom
+    return bb + t * (ba - bb)
+
+
+def merge_samples(z_c, z_f, *vals):
+    """Union of coarse (R,Nc) and fine (R,Nf) samples sorted by z, a coarse
+    sample first at equal z; vals are (coarse, fine) pairs gathered alike."""
+    R = z_f.shape[0]
+    zc = z_c.expand(R, -1) if z_c.dim() == 1 else z_c
+    z = torch.cat([zc, z_f], -1)
+    z_sorted, order = torch.sort(z, dim=-1, stable=True)
+    out = [z_sorted]
+    for vc, vf in vals:
+        v = torch.cat([vc, vf], 1)
+        idx = order.reshape(order.shape + (1,) * (v.dim() - 2)).expand(order.shape + v.shape[2:])
+        out.append(torch.gather(v, 1, idx))
+    return out
+
+
+def fine_image_step(p, shape_table, texture_table, obj_idx, ro, vd, z_c, z_f, gt, chunk=2048,
+                    reg_coef=1e-4, net=None):
+    """Coarse + fine training image (HIP: render.ImageStep.forward_backward_fine):
+    per chunk, loss = mean MSE of the coarse composite + mean MSE of the
+    composite over the merged coarse and fine samples (+ the code regulariser
+    on chunk 0), backward per chunk.  z_f (R, Nf) is given (from sample_pdf).
+    Returns (coarse losses, fine losses, fine rgb)."""
+    net = net or {}
+    Nc, Nf = z_c.shape[-1], z_f.shape[-1]
+    R = ro.shape[0]
+    lc_all, lf_all, outs = [], [], []
+    for a in range(0, R, chunk):
+        b = min(a + chunk, R)
+        s = shape_table[obj_idx][None]
+        t = texture_table[obj_idx][None]
+        zc = z_c if z_c.dim() == 1 else z_c[a:b]
+        xyz = ro[a:b, None, :] + vd[a:b, None, :] * zc[..., None]
+        sig_c, rgb_c = codenerf_forward(p, xyz, vd[a:b, None, :].expand(-1, Nc, -1), s, t, **net)
+        rgb, _ = volume_rendering(sig_c, rgb_c, zc)
+        l2c = torch.mean((rgb - gt[a:b]) ** 2)
+        zf = z_f[a:b]
+        xyz_f = ro[a:b, None, :] + vd[a:b, None, :] * zf[..., None]
+        sig_f, rgb_f = codenerf_forward(p, xyz_f, vd[a:b, None, :].expand(-1, Nf, -1), s, t, **net)
+        z_m, sig_m, rgb_m = merge_samples(zc, zf, (sig_c[..., 0], sig_f[..., 0]), (rgb_c, rgb_f))
+        rgb2, _ = volume_rendering(sig_m, rgb_m, z_m)
+        l2f = torch.mean((rgb2 - gt[a:b]) ** 2)
+        loss = l2c + l2f
+        if a == 0:
+            loss = loss + reg_coef * torch.mean(torch.norm(s, dim=-1) + torch.norm(t, dim=-1))
+        loss.backward()
+        lc_all.append(l2c.item())
+        lf_all.append(l2f.item())
+        outs.append(rgb2.detach())
+    return lc_all, lf_all, torch.cat(outs)
+
+
 class AdamWRef:
     """torch.optim.AdamW defaults as used at src/trainer.py:116-120
     (betas 0.9/0.999, eps 1e-8, weight_decay 0.01, no amsgrad), restated in
