@@ -100,18 +100,15 @@ def main():
 
     from codenerf_amd.model import CodeNeRF
     from codenerf_amd.trainer_core import TrainCore
+    from codenerf_amd.dp import broadcast_from, object_for
 
     torch.manual_seed(1234 + rank)
     model = CodeNeRF(3, 1, precision=args.precision).to(dev)
-    if dist is not None:      # identical initial weights on every rank
-        for p in model.parameters():
-            dist.broadcast(p.data, 0)
     n_obj = args.objects
     shape_codes = torch.nn.Parameter(torch.randn(n_obj, 256, device=dev) / math.sqrt(128))
     texture_codes = torch.nn.Parameter(torch.randn(n_obj, 256, device=dev) / math.sqrt(128))
-    if dist is not None:
-        dist.broadcast(shape_codes.data, 0)
-        dist.broadcast(texture_codes.data, 0)
+    # identical initial weights and codes on every rank
+    broadcast_from(list(model.parameters()) + [shape_codes, texture_codes], dist)
 
     H = W = args.H
     focal = 131.25 * H / 128
@@ -129,7 +126,7 @@ def main():
 
     def step(i):
         v = i % n_views
-        obj = (i * world + rank) % n_obj
+        obj = object_for(i, rank, world, n_obj)
         core.train_step(H, W, focal, poses[v], gts[v], obj)
 
     for i in range(args.warmup):

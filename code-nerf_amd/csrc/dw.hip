@@ -59,6 +59,10 @@ struct DwSeg {
   static constexpr int kRingStage = 8 * kG * 1024;
   static constexpr int kSmem = kBf16 ? (kDepth + 1) * kRingStage : 2 * kStage;
 
+  // FULL: a 256 x 256 layer (8 out tiles, 8 X tiles, no sigma head) -- the
+  // bulk of the bytes; every wave is live and the loop is branch-free, so
+  // the LDS reads of a k-step can be issued ahead of its MFMAs.
+  template <bool FULL>
   __device__ static void run(const DwProblem& pr, int t0, int t1, int rot, float* part, float* dbpart,
                              char* smem) {
     const int nst = t1 - t0;
@@ -72,13 +76,20 @@ struct DwSeg {
     const int wo = w >> 1, wi = w & 1;           // rows 64*wo.., cols 128*wi..
     const int h = lane >> 5;
     const int xt = pr.x0_tiles + pr.x1_tiles;    // staged X feature tiles
-    const bool extra = (wi == 0) && xt > 8;      // 9th X tile (dir PE) on the wi == 0 waves
-    const int a_bytes = pr.a_tiles * kTileB, x0_bytes = pr.x0_tiles * kTileB, x1_bytes = pr.x1_tiles * kTileB;
+    const bool extra = !FULL && (wi == 0) && xt > 8;   // 9th X tile (dir PE) on the wi == 0 waves
+    const int a_bytes = FULL ? 8 * kTileB : pr.a_tiles * kTileB;
+    const int x0_bytes = FULL ? 8 * kTileB : pr.x0_tiles * kTileB;
+    const int x1_bytes = FULL ? 0 : pr.x1_tiles * kTileB;
     const int stage_pieces = (a_bytes + x0_bytes + x1_bytes) >> 4;
-    const bool row0_live = 64 * wo < pr.out_tiles * 32;
-    const bool row1_live = 64 * wo + 32 < pr.out_tiles * 32;
-    const bool cols_live = 128 * wi < min(xt, 8) * 32;
-    const bool live = row0_live && (cols_live || extra);
+    const bool row0_live = FULL || 64 * wo < pr.out_tiles * 32;
+    const bool row1_live = FULL || 64 * wo + 32 < pr.out_tiles * 32;
+    const bool cols_live = FULL || 128 * wi < min(xt, 8) * 32;
+#ifdef CN_DW_NOCOMPUTE
+    const bool live = false;   // A/B measurement only: pure streaming
+#else
+    const bool live = FULL || (row0_live && (cols_live || extra));
+#endif
+    const bool sigma_head = !FULL && pr.sigma_head;
 
     f32x16 acc[2][5];
 #pragma unroll
@@ -211,7 +222,7 @@ struct DwSeg {
           }
         }
       }
-      if (pr.sigma_head) {
+      if (sigma_head) {
         // d w_sigma[f] += sum_s ds[s] * y[s][f];  ds = A[s][256] + A[s][257]
         const int f = threadIdx.x & 255;
         const int s0 = (threadIdx.x >> 8) * 16;
@@ -260,7 +271,7 @@ struct DwSeg {
         if (h == 0 && rl) dbpart[64 * wo + 32 * i + (lane & 31)] = tot;
       }
     }
-    if (pr.sigma_head) {
+    if (sigma_head) {
       // combine the two sample halves through LDS (the staging buffers are free now)
       float* red = (float*)smem;
       red[threadIdx.x] = sg;
@@ -287,7 +298,13 @@ __global__ __launch_bounds__(512, 2) void dw_kernel(DwArgs a) {
     dw_slab_range(a.wprefix, a.pbytes, a.total_tiles, p, b0, b1, t0, t1);
     if (t1 <= t0) continue;
     const size_t slot = (size_t)g * 2 + seg;
-    DwSeg<P>::run(a.p[p], t0, t1, g * 613, a.part + slot * kPartRows * kPartCols, a.dbpart + slot * kPartRows, smem);
+    const DwProblem& pr = a.p[p];
+    float* part = a.part + slot * kPartRows * kPartCols;
+    float* dbpart = a.dbpart + slot * kPartRows;
+    if (pr.out_tiles == 8 && pr.a_tiles == 8 && pr.x0_tiles == 8 && pr.x1_tiles == 0 && !pr.sigma_head)
+      DwSeg<P>::template run<true>(pr, t0, t1, g * 613, part, dbpart, smem);
+    else
+      DwSeg<P>::template run<false>(pr, t0, t1, g * 613, part, dbpart, smem);
     ++seg;
   }
 }

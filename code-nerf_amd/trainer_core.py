@@ -11,6 +11,7 @@ exchange is one RCCL all-reduce of 2.9 MB + the code tables per step.
 import torch
 
 from . import engine as _eng
+from .dp import GradBucket
 from .optim import FusedAdamW
 from .render import ImageStep
 
@@ -26,14 +27,8 @@ class TrainCore:
         self.n_fine = int(n_fine)
         self.dist = dist
         self.step_impl = ImageStep(model, chunk=chunk, reg_coef=reg_coef, timers=timers)
-        tensors = model.param_list() + [shape_codes, texture_codes]
-        total = sum(t.numel() for t in tensors)
-        dev = tensors[0].device
-        self.flat_grad = torch.zeros(total, dtype=torch.float32, device=dev)
-        off = 0
-        for t in tensors:
-            t.grad = self.flat_grad[off:off + t.numel()].view_as(t)
-            off += t.numel()
+        self.bucket = GradBucket(model.param_list() + [shape_codes, texture_codes])
+        self.flat_grad = self.bucket.flat
         self.opt = FusedAdamW([{"params": model.param_list(), "lr": lr[0]},
                                {"params": [shape_codes], "lr": lr[1]},
                                {"params": [texture_codes], "lr": lr[1]}])
@@ -48,7 +43,7 @@ class TrainCore:
         dev = c2w.device
         ro, vd = _eng.get_rays_dev(H, W, focal, True, c2w)
         z = self.stratified_z(dev)
-        self.flat_grad.zero_()
+        self.bucket.zero()
         if self.n_fine:
             rand_f = torch.rand(H * W, self.n_fine, device=dev)
             loss_c, loss_f, rgb, reg = self.step_impl.forward_backward_fine(
@@ -57,7 +52,6 @@ class TrainCore:
         else:
             losses, rgb, reg = self.step_impl.forward_backward(ro, vd, z, gt, self.shape_codes,
                                                                self.texture_codes, obj)
-        if self.dist is not None:
-            self.dist.all_reduce(self.flat_grad)
+        self.bucket.all_reduce(self.dist)
         self.opt.step()
         return losses, rgb
