@@ -207,6 +207,19 @@ int cn_mlp_dw(const cn_plan* p, void* d_act, int M, const float* d_zvec, float* 
   return launch_check("dw_reduce_kernel");
 }
 
+int cn_mlp_dbias(const cn_plan* p, void* d_act, int M, float* d_dbuf, void* d_ws, void* stream) {
+  if (!p || !d_act || !d_dbuf || !d_ws) return fail("cn_mlp_dbias: NULL argument");
+  if (M <= 0) return fail("cn_mlp_dbias: M must be positive");
+  DbArgs db;
+  p->cs.db_setup((char*)d_act, M, d_dbuf, (char*)d_ws, &db);
+  if (db.ninj <= 0) return 0;
+  if (p->cs.prec) hipLaunchKernelGGL(db_kernel<CN_P_BF16>, dim3(kDbBlocks, db.ninj), dim3(256), 0, S(stream), db);
+  else hipLaunchKernelGGL(db_kernel<CN_P_FP32>, dim3(kDbBlocks, db.ninj), dim3(256), 0, S(stream), db);
+  if (launch_check("db_kernel")) return -1;
+  hipLaunchKernelGGL(db_reduce_kernel, dim3(db.ninj), dim3(256), 0, S(stream), db);
+  return launch_check("db_reduce_kernel");
+}
+
 int cn_latent_bwd(const cn_plan* p, const float* const* d_params, float* const* d_grads, const float* d_shape,
                   const float* d_tex, const float* d_zvec, const float* d_dbuf, float* d_scratch, float* d_dshape,
                   float* d_dtex, float reg_coef, float* d_reg_out, void* stream) {

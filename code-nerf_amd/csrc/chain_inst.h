@@ -10,6 +10,7 @@ namespace cn {
 
 struct DwArgs;
 struct DwRedArgs;
+struct DbArgs;
 struct LatentArgs;
 struct LatentBwdArgs;
 
@@ -39,6 +40,8 @@ struct ChainSet {
   int (*dw_setup)(char* act, int M, const float* zvec, float* dbuf, char* ws, DwArgs* dw,
                   DwRedArgs* red) = nullptr;
   size_t (*dw_ws_bytes)(int M) = nullptr;
+  // fills the bias-only argument block (dbuf rows of the injection layers)
+  void (*db_setup)(char* act, int M, float* dbuf, char* ws, DbArgs* db) = nullptr;
 };
 
 ChainSet chain_set_fp32_3_1();

@@ -172,6 +172,28 @@ int dw_setup(char* act, int M, const float* zvec, float* dbuf, char* ws, DwArgs*
 }
 
 template <int P, int SB, int TB>
+void db_setup(char* act, int M, float* dbuf, char* ws, DbArgs* db) {
+  using N = Net<SB, TB>;
+  const int Mp = ((M + 255) / 256) * 256;
+  const ActLayout A = act_layout<P, SB, TB>(Mp);
+  static_assert(N::kInject <= kDbMaxInject, "injections");
+  *db = DbArgs{};
+  db->total_slabs = Mp / 32;
+  db->slabs_per_blk = (db->total_slabs + kDbBlocks - 1) / kDbBlocks;
+  int n = 0;
+  for (int L = 1; L < N::kFwdLayers; ++L) {
+    const int inj = N::fwd(L - 1).inj;
+    if (inj < 0) continue;
+    db->A[inj] = act + A.dA[L];
+    db->a_width[inj] = N::dplane_width(L);
+    ++n;
+  }
+  db->ninj = n;
+  db->part = (float*)ws;
+  db->dbout = dbuf;
+}
+
+template <int P, int SB, int TB>
 ChainSet make_chain_set() {
   using N = Net<SB, TB>;
   constexpr int WAVES = P == CN_P_BF16 ? 8 : 4;
@@ -198,6 +220,7 @@ ChainSet make_chain_set() {
   s.layout = act_layout<P, SB, TB>;
   s.dw_setup = dw_setup<P, SB, TB>;
   s.dw_ws_bytes = dw_ws_bytes<P, SB, TB>;
+  s.db_setup = db_setup<P, SB, TB>;
   return s;
 }
 

@@ -372,4 +372,30 @@ __global__ __launch_bounds__(256) void dw_reduce_kernel(DwRedArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- bias only
+template <int P>
+__global__ __launch_bounds__(256) void db_kernel(DbArgs a) {
+  using E = typename DwCfg<P>::E;
+  constexpr int ES = sizeof(E);
+  const int j = blockIdx.y, blk = blockIdx.x, f = threadIdx.x;
+  const int s0 = blk * a.slabs_per_blk, s1 = min(a.total_slabs, s0 + a.slabs_per_blk);
+  const char* A = (const char*)a.A[j];
+  const size_t slab_bytes = (size_t)a.a_width[j] * 32 * ES;
+  const int foff = f & ~3, fe = (f & 3) * ES;
+  float sum = 0.f;
+  for (int t = s0; t < s1; ++t) {
+    const char* base = A + (size_t)t * slab_bytes + fe;
+#pragma unroll 8
+    for (int s = 0; s < 32; ++s) sum += (float)*(const E*)(base + img_off<ES>(s, foff));
+  }
+  a.part[((size_t)j * kDbBlocks + blk) * 256 + f] = sum;
+}
+
+__global__ __launch_bounds__(256) void db_reduce_kernel(DbArgs a) {
+  const int j = blockIdx.x, f = threadIdx.x;
+  double sum = 0.0;
+  for (int b = 0; b < kDbBlocks; ++b) sum += a.part[((size_t)j * kDbBlocks + b) * 256 + f];
+  a.dbout[j * 256 + f] = (float)sum;
+}
+
 }  // namespace cn

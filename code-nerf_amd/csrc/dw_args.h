@@ -80,4 +80,18 @@ struct DwRedArgs {
   const float* dbpart;
 };
 
+// Bias gradients of the layers that follow a code injection only (codes-only
+// optimisation: no weight gradients needed): db_j = sum over samples of dA.
+constexpr int kDbMaxInject = 8;
+constexpr int kDbBlocks = 256;               // sample-range blocks per layer
+struct DbArgs {
+  const void* A[kDbMaxInject];               // dA plane of the layer after injection j
+  int a_width[kDbMaxInject];
+  int ninj;
+  int total_slabs;                           // Mp / 32
+  int slabs_per_blk;
+  float* part;                               // [ninj][kDbBlocks][256]
+  float* dbout;                              // [ninj][256]
+};
+
 }  // namespace cn

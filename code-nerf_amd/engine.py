@@ -8,6 +8,7 @@ on torch's current stream.  All arithmetic happens in the HIP library.
 import ctypes
 
 import torch
+from torch.autograd.graph import increment_version
 
 from . import _lib
 from ._lib import check, ptr
@@ -122,6 +123,11 @@ class Engine:
             ws = torch.empty(self.dw_ws_bytes(M), dtype=torch.uint8, device=self.device)
         check(self.L.cn_mlp_dw(self._plan, ptr(act), M, ptr(zvec), ptr(self.table(grads)), ptr(dbuf), ptr(ws),
                                self.stream), "cn_mlp_dw")
+
+    def mlp_dbias(self, act, M, dbuf, ws=None):
+        if ws is None:
+            ws = torch.empty(self.dw_ws_bytes(M), dtype=torch.uint8, device=self.device)
+        check(self.L.cn_mlp_dbias(self._plan, ptr(act), M, ptr(dbuf), ptr(ws), self.stream), "cn_mlp_dbias")
 
     def latent_bwd(self, params, grads, shape_code, texture_code, zvec, dbuf, d_shape, d_tex, reg_coef=0.0,
                    reg_out=None):
@@ -239,3 +245,7 @@ def adamw_step(params, grads, exp_avgs, exp_avg_sqs, lrs, weight_decay, beta1, b
     check(L.cn_adamw_step(n, ptrs(params), ptrs(grads), ptrs(exp_avgs), ptrs(exp_avg_sqs), counts, lr,
                           float(weight_decay), float(beta1), float(beta2), float(eps), int(step),
                           _dev_stream(params[0])), "cn_adamw_step")
+    # the kernel wrote the tensors behind torch's back: bump their version
+    # counters so version-keyed caches (the packed weights) see the update
+    increment_version(list(params))
+    increment_version(list(exp_avgs) + list(exp_avg_sqs))

@@ -43,9 +43,11 @@ class ImageStep:
         return [p.grad for p in tensors]
 
     def forward_backward(self, rays_o, viewdirs, z_vals, gt, shape_table, texture_table, obj_idx,
-                         reg=True):
+                         reg=True, weight_grads=True):
         """One image: returns (chunk losses [ceil(R/chunk)], rendered rgb [R,3],
-        reg loss [1]).  Gradients are accumulated into .grad."""
+        reg loss [1]).  Gradients are accumulated into .grad.  weight_grads
+        False (codes-only optimisation, src/optimizer.py): the weight-gradient
+        pass is replaced by the bias sums the code gradients need."""
         model = self.model
         eng = model.engine()
         params = model.param_list()
@@ -72,7 +74,11 @@ class ImageStep:
         if tm:
             tm.done("bwd", ev)
             ev = tm.mark("dw")
-        eng.mlp_dw(buf["act"], M, zvec, grads, buf["dbuf"], buf["dw"])
+        if weight_grads:
+            eng.mlp_dw(buf["act"], M, zvec, grads, buf["dbuf"], buf["dw"])
+        else:
+            eng.mlp_dbias(buf["act"], M, buf["dbuf"], buf["dw"])
+            grads = buf.setdefault("scratch_grads", [torch.zeros_like(p) for p in params])
         if tm:
             tm.done("dw", ev)
         reg_out = torch.zeros(1, dtype=torch.float32, device=eng.device)

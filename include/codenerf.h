@@ -92,6 +92,12 @@ int cn_mlp_bwd(const cn_plan *plan, const void *d_pack_bwd, const float *d_blob,
 int cn_mlp_dw(const cn_plan *plan, void *d_act, int M, const float *d_zvec,
               float *const *d_grads, float *d_dbuf, void *d_ws, void *stream);
 
+/* ---- bias gradients of the layers after each code injection only (d_dbuf
+ * [n_inject][256], as cn_mlp_dw writes them), for codes-only optimisation
+ * (src/optimizer.py:92: the model is fixed, only the codes are updated, so
+ * no weight gradients are needed).  d_ws: cn_dw_ws_bytes(plan, M) bytes. */
+int cn_mlp_dbias(const cn_plan *plan, void *d_act, int M, float *d_dbuf, void *d_ws, void *stream);
+
 /* ---- latent layers + code gradients (+ the code regulariser of
  * src/trainer.py:76-78 when reg_coef != 0; d_reg_out += reg value).
  * d_scratch: num_inject x 256 floats.  d_dshape / d_dtex accumulate. */
