@@ -133,6 +133,13 @@ int dw_setup(char* act, int M, const float* zvec, float* dbuf, char* ws, DwArgs*
     p.x0_tiles = p.x0_width / 32;
     if (vd) { p.X1 = act + A.dir; p.x1_width = 32; p.x1_tiles = 1; }
     p.sigma_head = vd ? 1 : 0;
+    p.kind = L == 0 ? DW_PE : vd ? DW_VIEWDIR : last ? DW_RGB2 : (L == N::kFwdLayers - 2 ? DW_RGB0 : DW_FULL);
+    {
+      // the bf16 bodies are compiled for exactly these operand shapes
+      static constexpr int shape[5][4] = {{8, 8, 0, 8}, {8, 2, 0, 8}, {9, 8, 1, 8}, {4, 8, 0, 4}, {1, 4, 0, 1}};
+      const int* e = shape[p.kind];
+      if (p.a_tiles != e[0] || p.x0_tiles != e[1] || p.x1_tiles != e[2] || p.out_tiles != e[3]) return -1;
+    }
     dw->pbytes[L] = (p.a_tiles + p.x0_tiles + p.x1_tiles) * 1024 * ES;
     dw->wprefix[L] = wsum;
     const long long tot = (long long)dw->pbytes[L] * dw->total_tiles;

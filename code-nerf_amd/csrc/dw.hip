@@ -84,8 +84,10 @@ struct DwSeg {
     const bool row0_live = FULL || 64 * wo < pr.out_tiles * 32;
     const bool row1_live = FULL || 64 * wo + 32 < pr.out_tiles * 32;
     const bool cols_live = FULL || 128 * wi < min(xt, 8) * 32;
-#ifdef CN_DW_NOCOMPUTE
+#if defined(CN_DW_NOCOMPUTE)
     const bool live = false;   // A/B measurement only: pure streaming
+#elif defined(CN_DW_FULLONLY)
+    const bool live = FULL;    // A/B measurement only: no compute on the ragged problems
 #else
     const bool live = FULL || (row0_live && (cols_live || extra));
 #endif
@@ -118,6 +120,9 @@ struct DwSeg {
     // the ring size so every slot offset is a compile-time constant.
     auto issue_dma = [&](int st, auto slotc) {
       char* dst = smem + decltype(slotc)::value * kRingStage;
+#ifdef CN_DW_NOLOAD
+      if (st >= 0) return;       // A/B measurement only: compute on stale LDS
+#endif
 #pragma unroll
       for (int k = 0; k < kG; ++k) {
         const int piece = w * kG + k;
@@ -286,9 +291,202 @@ struct DwSeg {
   }
 };
 
+// ------------------------------------------------------------ bf16 bodies
+// One compile-time body per operand shape (DwKind): every wave's tiles, LDS
+// reads, MFMAs and piece counts are constants, so the slab loop has no
+// runtime branches beyond wave-uniform role tests.  Staging: a 4-slot LDS-DMA
+// ring of 36 KiB slots, three slabs in flight while the fourth is consumed.
+template <int KIND> struct DwShape;
+//                                      A tiles, X0, X1, row tiles/wave, col tiles/wave
+template <> struct DwShape<DW_FULL>    { static constexpr int kA = 8, kX0 = 8, kX1 = 0, NI = 2, NJ = 4; };
+template <> struct DwShape<DW_PE>      { static constexpr int kA = 8, kX0 = 2, kX1 = 0, NI = 1, NJ = 2; };
+template <> struct DwShape<DW_VIEWDIR> { static constexpr int kA = 9, kX0 = 8, kX1 = 1, NI = 2, NJ = 4; };
+template <> struct DwShape<DW_RGB0>    { static constexpr int kA = 4, kX0 = 8, kX1 = 0, NI = 2, NJ = 2; };
+template <> struct DwShape<DW_RGB2>    { static constexpr int kA = 1, kX0 = 4, kX1 = 0, NI = 1, NJ = 1; };
+
+constexpr int kDwSlot = 36 * 1024;        // largest stage (viewdir: 18 tiles x 2 KiB)
+constexpr int kDwRing = 4;
+constexpr int kDwDepth = kDwRing - 1;     // slabs in flight while one is consumed
+constexpr int kDwDummy = kDwRing * kDwSlot;   // landing area of padding pieces (<= 6 KiB)
+constexpr int kDwSmemBf16 = kDwDummy + 8 * 1024;
+
+template <int KIND>
+struct DwBf16 {
+  using Sh = DwShape<KIND>;
+  static constexpr int kA = Sh::kA, kX0 = Sh::kX0, kX1 = Sh::kX1, NI = Sh::NI, NJ = Sh::NJ;
+  static constexpr int kPieces = 2 * (kA + kX0 + kX1);     // 1 KiB pieces per slab
+  static constexpr int kG = (kPieces + 7) / 8;              // pieces per wave per slab
+  static constexpr bool kVD = KIND == DW_VIEWDIR;
+  static_assert(kPieces * 1024 <= kDwSlot && (8 * kG - kPieces) * 1024 <= 8 * 1024, "dw stage");
+
+  // wave w's row tile i / column tile j (wave-uniform)
+  static CN_DEV int row_tile(int w, int i) {
+    if constexpr (KIND == DW_FULL || KIND == DW_VIEWDIR) return 2 * (w >> 1) + i;
+    else if constexpr (KIND == DW_PE) return w;
+    else if constexpr (KIND == DW_RGB0) return 2 * (w >> 2) + i;
+    else return 0;
+  }
+  static CN_DEV int col_tile(int w, int j) {
+    if constexpr (KIND == DW_FULL || KIND == DW_VIEWDIR) return 4 * (w & 1) + j;
+    else if constexpr (KIND == DW_PE) return j;
+    else if constexpr (KIND == DW_RGB0) return 2 * (w & 3) + j;
+    else return w;
+  }
+  static CN_DEV bool wave_live(int w) { return KIND != DW_RGB2 || w < 4; }
+  // the one wave per row tile that also sums the bias gradient (row sums of A)
+  static CN_DEV bool wave_db(int w) {
+    if constexpr (KIND == DW_FULL || KIND == DW_VIEWDIR) return (w & 1) == 0;
+    else if constexpr (KIND == DW_PE) return true;
+    else if constexpr (KIND == DW_RGB0) return (w & 3) == 0;
+    else return w == 0;
+  }
+
+  __device__ static void run(const DwProblem& pr, int t0, int t1, int rot, float* part, float* dbpart, char* smem) {
+    const int nst = t1 - t0;
+    rot %= nst;
+    auto slab = [&](int st) { const int t = st + rot; return t0 + (t >= nst ? t - nst : t); };
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int h = lane >> 5;
+    const bool live = wave_live(w);
+    const bool do_db = wave_db(w);
+
+    f32x16 acc[NI][NJ];
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x16{};
+    f32x16 acc_e1 = f32x16{}, acc_e2 = f32x16{};     // viewdir: (row w, dir tile), (sigma tile, col)
+    float dbacc[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) dbacc[i] = 0.f;
+    float dbsig = 0.f;
+
+    const char* pa = (const char*)pr.A;
+    const char* px0 = (const char*)pr.X0;
+    const char* px1 = kX1 ? (const char*)pr.X1 : px0;
+    auto issue = [&](int st, auto slotc) {
+      const size_t t = (size_t)slab(st);
+#pragma unroll
+      for (int k = 0; k < kG; ++k) {
+        const int piece = w * kG + k;            // wave-uniform
+        const char* src;
+        uint32_t dst = lds_addr(smem + decltype(slotc)::value * kDwSlot + piece * 1024);
+        if (piece < 2 * kA) src = pa + t * (kA * 2048) + piece * 1024;
+        else if (piece < 2 * (kA + kX0)) src = px0 + t * (kX0 * 2048) + (piece - 2 * kA) * 1024;
+        else if (piece < kPieces) src = px1 + t * (kX1 * 2048) + (piece - 2 * (kA + kX0)) * 1024;
+        else {
+          src = pa + t * (kA * 2048);            // padding piece: re-read, never consumed
+          dst = lds_addr(smem + kDwDummy + (piece - kPieces) * 1024);
+        }
+        glds16_opaque(src + lane * 16, dst);
+      }
+    };
+    static_for<0, kDwDepth>([&](auto i) {
+      if (i < nst) issue(i, i);
+    });
+
+    const int G = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    auto frag = [&](const char* base, int tile, int s) -> bf16x8 {
+      const int f = 32 * tile + 16 * (G & 1) + 4 * p;
+      s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + img_off<2>(s, f)));
+      s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + img_off<2>(s + 4, f)));
+      return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    auto rowsum = [](bf16x8 v) {
+      float sum = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sum += (float)v[j];
+      return sum;
+    };
+
+    auto body = [&](int st, auto slotc) {
+      constexpr int SL = decltype(slotc)::value;
+      const int ahead = min(kDwDepth - 1, nst - 1 - st);
+      static_for<0, kDwDepth>([&](auto n) {
+        if (n == ahead) wait_vmcnt<n * kG>();
+      });
+      block_barrier();
+      if (st + kDwDepth < nst) issue(st + kDwDepth, std::integral_constant<int, (SL + kDwDepth) % kDwRing>{});
+      const char* A = smem + SL * kDwSlot;
+      const char* X = A + kA * 2048;
+      if (!live) return;
+#pragma unroll
+      for (int kk = 0; kk < 32; kk += 16) {
+        const int s = kk + 8 * h + q;
+        bf16x8 fa[NI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+          fa[i] = frag(A, row_tile(w, i), s);
+          if (do_db) dbacc[i] += rowsum(fa[i]);
+        }
+        bf16x8 fs{};
+        if constexpr (kVD) {
+          fs = frag(A, 8, s);                    // sigma-head columns 256.. of the dA plane
+          if (w == 0) dbsig += rowsum(fs);
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const bf16x8 fx = frag(X, col_tile(w, j), s);
+#pragma unroll
+          for (int i = 0; i < NI; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fx, acc[i][j], 0, 0, 0);
+          if constexpr (kVD) {
+            if (j == (w >> 1)) acc_e2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fs, fx, acc_e2, 0, 0, 0);
+          }
+        }
+        if constexpr (kVD) {
+          const bf16x8 fd = frag(X, 8, s);       // dir-PE input tile
+          const bf16x8 fr = (w & 1) ? fa[1] : fa[0];
+          acc_e1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr, fd, acc_e1, 0, 0, 0);
+        }
+      }
+    };
+    for (int base = 0; base < nst; base += kDwRing)
+      static_for<0, kDwRing>([&](auto k) {
+        if (base + k < nst) body(base + k, k);
+      });
+    __syncthreads();
+
+    // ---- fp32 partial: row n (out feature), column c (in feature)
+    if (live) {
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int col = 32 * col_tile(w, j) + (lane & 31);
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            part[(size_t)(32 * row_tile(w, i) + acc_row(r, h)) * kPartCols + col] = acc[i][j][r];
+        }
+      if constexpr (kVD) {
+        const int col = 256 + (lane & 31);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) part[(size_t)(32 * w + acc_row(r, h)) * kPartCols + col] = acc_e1[r];
+        // sigma head: d w_sigma = sum_s (dA[256] + dA[257]) x y: rows 0 and 1 of the sigma tile
+        if (h == 0) part[(size_t)256 * kPartCols + 32 * (4 * (w & 1) + (w >> 1)) + (lane & 31)] = acc_e2[0] + acc_e2[1];
+      }
+    }
+    if (do_db && live) {
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const float tot = dbacc[i] + __shfl_xor(dbacc[i], 32);
+        if (h == 0) dbpart[32 * row_tile(w, i) + (lane & 31)] = tot;
+      }
+    }
+    if constexpr (kVD) {
+      if (w == 0) {
+        const float tot = dbsig + __shfl_xor(dbsig, 32);
+        const float both = tot + __shfl(tot, 1);
+        if (lane == 0) dbpart[256] = both;
+      }
+    }
+    __syncthreads();
+  }
+};
+
 template <int P>
 __global__ __launch_bounds__(512, 2) void dw_kernel(DwArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[DwSeg<P>::kSmem];
+  __shared__ __attribute__((aligned(16))) char smem[P == CN_P_BF16 ? kDwSmemBf16 : DwSeg<P>::kSmem];
   const int g = blockIdx.x;
   const long long total = a.wprefix[a.nprob];
   const long long b0 = dw_share_begin(g, total, a.nwg), b1 = dw_share_begin(g + 1, total, a.nwg);
@@ -301,10 +499,19 @@ __global__ __launch_bounds__(512, 2) void dw_kernel(DwArgs a) {
     const DwProblem& pr = a.p[p];
     float* part = a.part + slot * kPartRows * kPartCols;
     float* dbpart = a.dbpart + slot * kPartRows;
-    if (pr.out_tiles == 8 && pr.a_tiles == 8 && pr.x0_tiles == 8 && pr.x1_tiles == 0 && !pr.sigma_head)
+    if constexpr (P == CN_P_BF16) {
+      switch (pr.kind) {
+        case DW_FULL: DwBf16<DW_FULL>::run(pr, t0, t1, g * 613, part, dbpart, smem); break;
+        case DW_PE: DwBf16<DW_PE>::run(pr, t0, t1, g * 613, part, dbpart, smem); break;
+        case DW_VIEWDIR: DwBf16<DW_VIEWDIR>::run(pr, t0, t1, g * 613, part, dbpart, smem); break;
+        case DW_RGB0: DwBf16<DW_RGB0>::run(pr, t0, t1, g * 613, part, dbpart, smem); break;
+        default: DwBf16<DW_RGB2>::run(pr, t0, t1, g * 613, part, dbpart, smem); break;
+      }
+    } else if (pr.out_tiles == 8 && pr.a_tiles == 8 && pr.x0_tiles == 8 && pr.x1_tiles == 0 && !pr.sigma_head) {
       DwSeg<P>::template run<true>(pr, t0, t1, g * 613, part, dbpart, smem);
-    else
+    } else {
       DwSeg<P>::template run<false>(pr, t0, t1, g * 613, part, dbpart, smem);
+    }
     ++seg;
   }
 }

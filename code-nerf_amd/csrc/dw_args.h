@@ -20,6 +20,17 @@ struct DwProblem {
   int x1_width, x1_tiles;
   int sigma_head;       // viewdir: also sum ds (A column 256 + 257) x X columns 0..255
   int rows_pad, cols_pad;   // extent of the partial actually written (<= 288)
+  int kind;             // DwKind: operand shape, selects the compile-time bf16 body
+};
+
+// The five operand shapes of the CodeNeRF weight gradients (tiles of 32
+// features: A = gradient plane, X = input plane(s)).
+enum DwKind : int {
+  DW_FULL = 0,      // 256 x 256 hidden layers             A 8, X 8
+  DW_PE = 1,        // encoding_xyz: 256 x 63 (PE input)   A 8, X 2
+  DW_VIEWDIR = 2,   // encoding_viewdir (+ sigma head)     A 9, X 8 + 1 (dir PE)
+  DW_RGB0 = 3,      // rgb.0: 128 x 256                    A 4, X 8
+  DW_RGB2 = 4,      // rgb.2: 3 x 128                      A 1, X 4
 };
 
 // Persistent, byte-balanced schedule: the (problem, slab) stream -- problem

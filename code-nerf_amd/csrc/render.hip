@@ -378,6 +378,11 @@ __global__ __launch_bounds__(256) void fine_render_loss_kernel(
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
+  // Every merged slot starts as "no source": with non-finite z (diverged
+  // weights) the two rank computations below need not form a permutation, and
+  // an unwritten slot must not scatter through an undefined index.
+  for (int p = lane; p < N; p += 64) m_src[wv][p] = -1;
+  wave_sync();
   // merged position = own index + number of the other list's samples before it
   for (int i = lane; i < Nc; i += 64) {
     const float v = zcr[i];
@@ -429,6 +434,7 @@ __global__ __launch_bounds__(256) void fine_render_loss_kernel(
   wave_sync();
   for (int p = lane; p < N; p += 64) {
     const int src = m_src[wv][p];
+    if (src < 0) continue;
     if (src < Nc) {
       const size_t g = (size_t)r * Nc + src;
       dsig_c[g] += m_dsig[wv][p];

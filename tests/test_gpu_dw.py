@@ -1,0 +1,177 @@
+"""Weight-gradient pass (dw_kernel + dw_reduce_kernel) against a float64
+reduction of the very operands it reads.
+
+The chain kernels leave the layer inputs X and output gradients dA in the
+activation workspace (wave-tiled planes, csrc/cn_layout.h).  This test decodes
+those planes with torch indexing, forms every weight / bias gradient of the
+reference parameter set (src/model.py:11-34) as sum_m dA[m] (x) (X[m] + u) in
+float64 (u = the folded code injection, src/model.py:41-43,49-51), and checks
+the kernel's fp32 result to accumulation-order tolerance.  Both precisions;
+M ragged, so the padded tail samples are covered (their dA must be zero).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+SB, TB = 3, 1
+N_PLANES = SB + TB + 4
+
+
+def plane_width(p):
+    return 128 if p == SB + TB + 3 else 256
+
+
+def dplane_width(p):
+    return 128 if p == SB + TB + 3 else (288 if p == SB + 2 else 256)
+
+
+def act_offsets(Mp, es):
+    """Byte offsets of the workspace planes (restates act_layout, csrc/chain_set.h)."""
+    off = 0
+    out = {}
+
+    def take(name, n):
+        nonlocal off
+        out[name] = off
+        off += (n + 255) & ~255
+
+    take("pe", Mp * 64 * es)
+    take("dir", Mp * 32 * es)
+    for p in range(N_PLANES):
+        take(f"Y{p}", Mp * plane_width(p) * es)
+    for p in range(N_PLANES):
+        take(f"dA{p}", Mp * dplane_width(p) * es)
+    take("d8", Mp * 32 * es)
+    return out
+
+
+def decode(act, off, F, Mp, dtype):
+    """(Mp, F) float64 view of a wave-tiled plane (plane_off, csrc/cn_layout.h)."""
+    es = torch.finfo(dtype).bits // 8
+    dev = act.device
+    m = torch.arange(Mp, device=dev)[:, None]
+    f = torch.arange(F, device=dev)[None, :]
+    g, hh, s = (f >> 3) & 3, (f >> 2) & 1, m & 31
+    pos = ((s + 8 * g + 4 * hh) & 31) + 32 * hh
+    elem = ((((m >> 5) * (F >> 5) + (f >> 5)) * 4 + g) * 256 + pos * 4 + (f & 3))
+    flat = act[off:off + Mp * F * es].view(dtype)
+    return flat[elem].double()
+
+
+def pe_slot_feature(h, s):
+    if s == 0:
+        return 0 if h == 0 else 2
+    if s == 1:
+        return 1 if h == 0 else -1
+    k = (s - 2) >> 1
+    p = 15 * h + k
+    return 3 + p if (s & 1) == 0 else 33 + p
+
+
+def dir_slot_feature(h, s):
+    if s == 0:
+        return 0 if h == 0 else 2
+    if s == 1:
+        return 1 if h == 0 else -1
+    k = (s - 2) >> 1
+    p = k if h == 0 else 7 + k
+    if h == 1 and k >= 5:
+        return -1
+    return 3 + p if (s & 1) == 0 else 15 + p
+
+
+def col_feature(fn, c):
+    return fn((c >> 2) & 1, 4 * (c >> 3) + (c & 3))
+
+
+def scatter_cols(dw_cols, fn, n_real):
+    """Partial columns (plane order) -> reference input features."""
+    out = torch.zeros(dw_cols.shape[0], n_real, dtype=torch.float64, device=dw_cols.device)
+    for c in range(dw_cols.shape[1]):
+        f = col_feature(fn, c)
+        if f >= 0:
+            out[:, f] += dw_cols[:, c]
+    return out
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+def test_weight_gradients_match_float64_reduction(precision):
+    from codenerf_amd.model import CodeNeRF
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(3)
+    m = CodeNeRF(SB, TB, precision=precision).to(dev)
+    eng = m.engine()
+    params = m.param_list()
+    names = [n for n, _ in m.named_parameters()]
+    R, N = 3000 - 7, 64                      # ragged: M not a multiple of 256
+    M = R * N
+    ro = torch.zeros(R, 3, device=dev) + torch.tensor([0.0, 0.4, 1.2], device=dev)
+    vd = torch.nn.functional.normalize(torch.randn(R, 3, device=dev) * 0.2 + torch.tensor([0., -0.3, -1.], device=dev),
+                                       dim=-1)
+    z = torch.linspace(0.8, 1.8, N, device=dev)
+    s = torch.randn(256, device=dev) / 11.3
+    t = torch.randn(256, device=dev) / 11.3
+    eng.ensure_packed(params, bwd=True)
+    blob, zvec = eng.latent_fwd(params, s, t)
+    act = eng.new_act(M)
+    eng.mlp_fwd(blob, M, rays_o=ro, rays_d=vd, z=z, n_samples=N, act=act)
+    Mp = eng.pad(M)
+    dsig = torch.zeros(Mp, device=dev)
+    drgb = torch.zeros(Mp, 3, device=dev)
+    dsig[:M] = torch.randn(M, device=dev) * 1e-3
+    drgb[:M] = torch.randn(M, 3, device=dev) * 1e-3
+    eng.mlp_bwd(blob, M, dsig, drgb, act)
+    grads = [torch.zeros_like(p) for p in params]
+    dbuf = torch.zeros(eng.n_inject, 256, device=dev)
+    eng.mlp_dw(act, M, zvec, grads, dbuf)
+    torch.cuda.synchronize()
+    G = dict(zip(names, grads))
+
+    dtype = torch.bfloat16 if precision == "bf16" else torch.float32
+    es = 2 if precision == "bf16" else 4
+    off = act_offsets(Mp, es)
+    Y = [decode(act, off[f"Y{p}"], plane_width(p), Mp, dtype) for p in range(N_PLANES)]
+    dA = [decode(act, off[f"dA{p}"], dplane_width(p), Mp, dtype) for p in range(N_PLANES)]
+    d8 = decode(act, off["d8"], 32, Mp, dtype)
+    pe = decode(act, off["pe"], 64, Mp, dtype)
+    dr = decode(act, off["dir"], 32, Mp, dtype)
+    for a in dA + [d8]:
+        assert torch.count_nonzero(a[M:]) == 0, "padded samples must carry no gradient"
+    u = zvec.double()
+
+    def check(name, ref):
+        got = G[name].double()
+        scale = ref.abs().max().item()
+        err = (got - ref).abs().max().item()
+        assert err <= 1e-4 * scale + 1e-12, f"{name}: max err {err:.3e} vs scale {scale:.3e}"
+
+    # (weight name, A, X, injection index or None) in forward order, src/model.py:36-53
+    layers = [("encoding_xyz.0", dA[0], None, None)]
+    for j in range(1, SB + 1):
+        layers.append((f"shape_layer_{j}.0", dA[j], Y[j - 1], j - 1))
+    layers.append(("encoding_shape", dA[SB + 1], Y[SB], None))
+    layers.append(("texture_layer_1.0", dA[SB + 3], Y[SB + 2], SB))
+    layers.append(("rgb.0", dA[SB + TB + 3], Y[SB + TB + 2], None))
+    layers.append(("rgb.2", d8[:, :3], Y[SB + TB + 3], None))
+    for name, A, X, inj in layers:
+        if name == "encoding_xyz.0":
+            ref = scatter_cols(A.T @ pe, pe_slot_feature, 63)
+        else:
+            Xu = X + (u[inj][None, :] if inj is not None else 0.0)
+            ref = A.T @ Xu
+        check(name + ".weight", ref)
+        check(name + ".bias", A.sum(0))
+        if inj is not None:
+            np.testing.assert_allclose(dbuf[inj].double().cpu().numpy(), A.sum(0).cpu().numpy(),
+                                       rtol=1e-4, atol=1e-4 * A.sum(0).abs().max().item())
+    # encoding_viewdir: input [y_shape (256) | dir PE (27)]; the dA plane's
+    # columns 256 + 257 carry the sigma-head gradient ds
+    A5 = dA[SB + 2]
+    ref = torch.cat([A5[:, :256].T @ Y[SB + 1], scatter_cols(A5[:, :256].T @ dr, dir_slot_feature, 27)], dim=1)
+    check("encoding_viewdir.0.weight", ref)
+    check("encoding_viewdir.0.bias", A5[:, :256].sum(0))
+    ds = A5[:, 256] + A5[:, 257]
+    check("sigma.0.weight", (ds[None, :] @ Y[SB + 1]))
+    check("sigma.0.bias", ds.sum().reshape(1))
