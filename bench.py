@@ -30,6 +30,7 @@ BF16_PEAK_TFLOPS = 2500.0       # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 FP32_PEAK_TFLOPS = 157.3        # fp32 MFMA
 HBM_PEAK_GBS = 8000.0
 FLOP_PER_SAMPLE = {"fwd": 899_328, "bwd": 853_248, "dw": 899_328}
+DW_BYTES_PER_SAMPLE = 8_000     # bf16 dA + X operand planes read by dw_kernel
 
 
 def parse():
@@ -164,6 +165,16 @@ def main():
                 "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": load_traffic(dom),
                 "ms_per_launch": {k: round(v, 4) for k, v in kern.items()}}
+        if dom == "dw" and args.precision == "bf16":
+            # the weight-gradient pass streams the stored bf16 operands (dA and X
+            # planes, 8,000 B per sample at the srncar net): its practical limiter
+            dw_bytes = DW_BYTES_PER_SAMPLE * samples_per_step
+            gbs = dw_bytes / (kern["dw"] * 1e-3) / 1e9
+            roof["hbm_view"] = {"bytes_per_launch": dw_bytes, "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                                "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
+        step_flops = sum(FLOP_PER_SAMPLE.values()) * samples_per_step
+        roof["step"] = {"achieved": round(step_flops / (ms * 1e-3) / 1e12, 2), "unit": "TFLOP/s",
+                        "frac": round(step_flops / (ms * 1e-3) / 1e12 / peak, 4)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

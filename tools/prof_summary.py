@@ -26,7 +26,7 @@ def short(name):
 
 def counters(d, counter):
     out = {}
-    for fn in glob.glob(os.path.join(d, "*counter_collection.csv")):
+    for fn in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(fn)):
             if r["Counter_Name"] == counter:
                 out.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
@@ -38,7 +38,7 @@ def main():
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     prof = os.path.join(repo, "profiles")
     os.makedirs(prof, exist_ok=True)
-    stats = list(csv.DictReader(open(glob.glob(os.path.join(stats_dir, "*kernel_stats.csv"))[0])))
+    stats = list(csv.DictReader(open(glob.glob(os.path.join(stats_dir, "**", "*kernel_stats.csv"), recursive=True)[0])))
     fetch, write = counters(fetch_dir, "FETCH_SIZE"), counters(write_dir, "WRITE_SIZE")
     lines = [f"# rocprofv3 --kernel-trace --stats ({tag})", "",
              "| kernel | calls | avg us | % time | FETCH_SIZE KiB | WRITE_SIZE KiB | HBM GB/launch (2F+W) | GB/s |",
