@@ -50,6 +50,30 @@ CN_DEV uint32_t relu_bf16x2(uint32_t x) {
   v = __builtin_elementwise_max(v, s16x2{0, 0});
   return __builtin_bit_cast(uint32_t, v);
 }
+// ReLU backward from the stored sign bits (bit set -> pre-activation < 0 ->
+// gradient 0).  fp32: one element.  bf16: a packed pair (elements at bit
+// positions pa (low half) and pb (high half)) masked AFTER packing: the
+// 16-bit halves of the mask are built with one v_bfi_b32 and applied with one
+// v_and_b32 -- a plain AND on a packed word, which the compiler cannot turn
+// into the v_cmp + v_cndmask (+ VCC hazard nop) it emits for a per-element
+// masked select.  Masking before or after the bf16 rounding is the same.
+CN_DEV float relu_mask(float v, uint32_t word, int pos) {
+  const uint32_t off = (uint32_t)__builtin_amdgcn_sbfe((int)word, pos, 1);
+  return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, v) & ~off);
+}
+template <int PA, int PB>
+CN_DEV uint32_t relu_mask_bf16x2(uint32_t p, uint32_t word) {
+  // the pair mask is built in asm (two sign-extended bit extracts, halves
+  // merged by v_bfi): the compiler would rewrite a sign-extended bit into
+  // v_and + v_cmp + v_cndmask.  The final AND stays compiler-visible, so the
+  // hazard recognizer sees the VALU write that feeds the next MFMA.
+  uint32_t m2, tmp;
+  asm("v_bfe_i32 %0, %2, %3, 1\n\t"
+      "v_bfe_i32 %1, %2, %4, 1\n\t"
+      "v_bfi_b32 %0, %5, %0, %1"
+      : "=&v"(m2), "=&v"(tmp) : "v"(word), "I"(PA), "I"(PB), "s"(0xFFFFu));
+  return p & ~m2;
+}
 // shift the sign bit of v into the running mask word (one v_alignbit_b32)
 CN_DEV uint32_t push_sign(uint32_t bits, float v) {
   return __builtin_amdgcn_alignbit(bits, __builtin_bit_cast(uint32_t, v), 31);
@@ -61,14 +85,29 @@ CN_DEV uint32_t push_sign(uint32_t bits, float v) {
 template <class E>
 CN_DEV void plane_store(__amdgpu_buffer_rsrc_t r, const uint32_t* voff, int F, int wglob, int t, int g,
                         float a, float b, float c, float d) {
-  const int soff = ((wglob * (F >> 5) + t) * 4 + g) * (256 * (int)sizeof(E));
+  const int soff = (wglob * (F >> 5) + t) * (1024 * (int)sizeof(E));
   bstore4<E>(r, voff[g], soff, a, b, c, d);
 }
-template <class E>
-CN_DEV void plane_store_packed(__amdgpu_buffer_rsrc_t r, const uint32_t* voff, int F, int wglob, int t, int g,
-                               u32x2 v) {
-  const int soff = ((wglob * (F >> 5) + t) * 4 + g) * (256 * (int)sizeof(E));
-  bstore64(r, voff[g], v, soff);
+// bf16: groups 2gp and 2gp+1 of feature tile t (this lane: 4 + 4 features as
+// packed pairs) -> one 16-B store per lane.  v_permlane32_swap exchanges the
+// upper half's group-2gp dwords with the lower half's group-(2gp+1) dwords, so
+// lane s holds features 16gp .. 16gp+7 and lane s+32 features 16gp+8 .. +15 of
+// sample s, which is the bf16 pair-block layout (cn_layout.h); voff16 =
+// bf16_pos(s, gp, h) * 16 + gp * 1024.
+//
+// Hazard (observed on gfx950, ROCm 7.2, not flagged by the compiler): a
+// buffer store whose data comes straight from v_permlane32_swap reads its
+// first data dword late, after the NEXT VALU instruction has already
+// rewritten that register.  The data therefore passes through an asm
+// barrier with wait states before the store, and stays live through a second
+// one after it, so no VALU can reuse those registers inside the window.
+CN_DEV void plane_store_pair(__amdgpu_buffer_rsrc_t r, uint32_t voff16, int F, int wglob, int t, u32x2 a, u32x2 b) {
+  const auto x = __builtin_amdgcn_permlane32_swap(a[0], b[0], false, false);
+  const auto y = __builtin_amdgcn_permlane32_swap(a[1], b[1], false, false);
+  u32x4 d = u32x4{x[0], y[0], x[1], y[1]};
+  asm volatile("s_nop 3" : "+v"(d));
+  bstore128(r, voff16, d, (wglob * (F >> 5) + t) * 2048);
+  asm volatile("s_nop 1" ::"v"(d) : "memory");
 }
 
 template <int P, int SB, int TB, bool BWD, int WAVES, bool TRAIN>
@@ -82,8 +121,18 @@ struct Chain {
   static constexpr int NL = S::NL;
   static constexpr int kChunks = S::kChunks;
   static constexpr int G = kChunkBlocks / WAVES;   // LDS-DMA instructions per wave per chunk
-  static constexpr int D = 3;                      // chunks in flight ahead of compute
+#ifndef CN_CHAIN_DF
+#define CN_CHAIN_DF 3
+#endif
+#ifndef CN_CHAIN_DB
+#define CN_CHAIN_DB 2
+#endif
+  static constexpr int D = BWD ? CN_CHAIN_DB : CN_CHAIN_DF;   // chunks in flight ahead of compute
   static constexpr int NS = D + 1;                 // ring slots
+#ifndef CN_CHAIN_PF
+#define CN_CHAIN_PF 2
+#endif
+  static constexpr int kPF = CN_CHAIN_PF;          // bf16 A-fragment prefetch distance (blocks)
   static constexpr int kRingBytes = NS * kChunkBytes;
   static constexpr int kBlobFloats = BiasBlob<SB, TB>::kFloats;
   static constexpr int kWsOff = BiasBlob<SB, TB>::kWs;
@@ -97,23 +146,48 @@ struct Chain {
   static_assert(N::kPlanes <= kMaxPlanes, "too many planes");
   static_assert(kBlobFloats % 4 == 0, "blob alignment");
 
+  // ---------------- deferred plane stores (bf16)
+  // A layer's output plane (Y forward, dA backward) is exactly the packed B
+  // operand `bin` of the NEXT layer, so its 16-B pair stores are issued
+  // spread over the next layer's MFMA blocks instead of as one burst in the
+  // epilogue (where every wave of the workgroup would stall on its store
+  // queue at the same time).  Store j of layer li-1 follows block
+  // first_block(li) + j * lblocks(li) / n.  The last layer's plane (backward:
+  // dA of the first forward layer) has no next layer and is stored in place.
+  static constexpr bool plane_of(int i) { return BWD ? true : (TRAIN && S::L(i).plane >= 0); }
+  static constexpr bool defers(int i) { return kBf16 && plane_of(i) && i + 1 < NL; }
+  static constexpr int deferred_count(int i) { return defers(i) ? 2 * S::L(i).T : 0; }
+  // index j of the deferred store of layer li-1 issued after block g, or -1
+  static constexpr int deferred_at(int g) {
+    const int li = S::layer_of(g);
+    if (li == 0) return -1;
+    const int n = deferred_count(li - 1);
+    if (n == 0) return -1;
+    const int nb = S::lblocks(li), lb = g - S::first_block(li);
+    for (int j = 0; j < n; ++j)
+      if (j * nb / n == lb) return j;
+    return -1;
+  }
+
   // ---------------- compile-time vmcnt bookkeeping
-  // Number of vector-memory instructions each wave issues in a layer epilogue.
+  // Vector-memory instructions each wave issues in a layer epilogue.
   static constexpr int stores_of_layer(int i) {
     const Layer l = S::L(i);
     if (!BWD) {
       int s = 0;
-      if (TRAIN && l.plane >= 0) s += l.T * 4;
+      if (plane_of(i) && !defers(i)) s += l.T * (kBf16 ? 2 : 4);
       if (TRAIN && l.mask >= 0) s += 1;
       if (l.epi == EPI_SHAPE) s += TRAIN ? 2 : 1;
       return s;   // EPI_RGB stores come after the last wait: not counted (safe)
     }
-    return l.T * 4;
+    return defers(i) ? 0 : l.T * (kBf16 ? 2 : 4);
   }
   static constexpr int stores_in_chunk(int c) {
     int s = 0;
     for (int i = 0; i < NL; ++i)
       if (S::last_block(i) / kChunkBlocks == c) s += stores_of_layer(i);
+    for (int g = c * kChunkBlocks; g < (c + 1) * kChunkBlocks && g < S::kBlocks; ++g)
+      if (deferred_at(g) >= 0) s += 1;
     return s;
   }
   static constexpr int issued(int i) { return i < kChunks ? G : 0; }
@@ -140,9 +214,11 @@ struct Chain {
     const int mc = m < a.M ? m : a.M - 1;
     const int wglob = blockIdx.x * WAVES + w;
     float* prm = (float*)(smem + kRingBytes);
-    uint32_t voff[4];
+    uint32_t voff[6];   // [g]: 8-B stores of group g; [4 + gp]: bf16 16-B pair stores
 #pragma unroll
-    for (int g = 0; g < 4; ++g) voff[g] = (uint32_t)tile_pos(lane & 31, g, h) * (4 * sizeof(E));
+    for (int g = 0; g < 4; ++g) voff[g] = (uint32_t)slab_off(lane & 31, 8 * g + 4 * h, (int)sizeof(E));
+#pragma unroll
+    for (int gp = 0; gp < 2; ++gp) voff[4 + gp] = (uint32_t)(bf16_pos(lane & 31, gp, h) * 16 + gp * 1024);
 
     // -- per-call bias blob -> LDS (plain loads; nothing is in flight yet)
     for (int i = threadIdx.x; i < kBlobFloats / 4; i += WAVES * 64)
@@ -167,12 +243,16 @@ struct Chain {
     static_for<0, D>([&](auto i) { issue<i>(a, smem, w, lane); });
 
     float sig_part = 0.f;
-    static_for<0, kChunks>([&](auto cc) {
+    auto chunk = [&](auto cc) {
       constexpr int c = cc;
-      wait_vmcnt<vm_wait(c)>();
-      block_barrier();
-      if constexpr (c + D < kChunks) issue<c + D>(a, smem, w, lane);
       const char* slot = smem + (c % NS) * kChunkBytes + lane * 16;
+      // bf16: A fragments are read kPF blocks ahead of their MFMA (rolling
+      // register buffer), so the LDS latency hides behind earlier MFMAs
+      bf16x8 Abuf[kPF + 1];
+      if constexpr (kBf16)
+        static_for<0, kPF>([&](auto bb) {
+          if constexpr (c * kChunkBlocks + bb < S::kBlocks) Abuf[bb] = *(const bf16x8*)(slot + bb * kBlockBytes);
+        });
       static_for<0, kChunkBlocks>([&](auto bb) {
         constexpr int g = c * kChunkBlocks + bb;
         if constexpr (g < S::kBlocks) {
@@ -182,9 +262,10 @@ struct Chain {
           constexpr int kb = lb % S::bpt(li);
           const char* ap = slot + bb * kBlockBytes;
           if constexpr (kBf16) {
-            const bf16x8 A = *(const bf16x8*)ap;
+            if constexpr (bb + kPF < kChunkBlocks && g + kPF < S::kBlocks)
+              Abuf[(bb + kPF) % (kPF + 1)] = *(const bf16x8*)(ap + kPF * kBlockBytes);
             acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                A, __builtin_bit_cast(bf16x8, bin[kb]), acc[t], 0, 0, 0);
+                Abuf[bb % (kPF + 1)], __builtin_bit_cast(bf16x8, bin[kb]), acc[t], 0, 0, 0);
           } else {
             const f32x4 A = *(const f32x4*)ap;
             acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[0], bin[4 * kb + 0], acc[t], 0, 0, 0);
@@ -198,8 +279,24 @@ struct Chain {
             else
               epilogue_bwd<li>(a, bin, acc, prm, smem, h, lane, w, m, wglob, voff, ds);
           }
+          if constexpr (deferred_at(g) >= 0) {
+            constexpr int j = deferred_at(g);
+            constexpr int pl = li - 1;                 // layer whose output bin holds
+            constexpr int plane = S::L(pl).plane;
+            constexpr int F = BWD ? N::dplane_width(plane) : N::plane_width(plane);
+            const u32x4 b = bin[j];                    // tile j / 2, pair j % 2
+            plane_store_pair(mkrsrc(BWD ? a.dA[plane] : a.Y[plane]), voff[4 + (j & 1)], F, wglob, j >> 1,
+                             u32x2{b[0], b[1]}, u32x2{b[2], b[3]});
+          }
         }
       });
+    };
+    static_for<0, kChunks>([&](auto kk) {
+      constexpr int k = kk;
+      wait_vmcnt<vm_wait(k)>();
+      block_barrier();
+      if constexpr (k + D < kChunks) issue<k + D>(a, smem, w, lane);
+      chunk(std::integral_constant<int, k>{});
     });
   }
 
@@ -255,7 +352,11 @@ struct Chain {
       const int comp = p % 3, oct = p / 3;
       const float v = (comp == 0 ? x[0] : comp == 1 ? x[1] : x[2]) * (float)(1 << oct);
       float sn, cs;
+#ifdef CN_FAST_PE
+      sn = __sinf(v); cs = __cosf(v);      // A/B measurement only: inaccurate for large |v|
+#else
       sincosf(v, &sn, &cs);
+#endif
       pe[2 + 2 * k] = sn;
       pe[3 + 2 * k] = cs;
     }
@@ -370,9 +471,9 @@ struct Chain {
       const float* ws = prm + kWsOff + 4 * h;
 #pragma unroll
       for (int t = 0; t < l.T; ++t) {
+        u32x2 pg[4];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const int row0 = 32 * t + 8 * g + 4 * h;
           float v0 = acc[t][4 * g + 0], v1 = acc[t][4 * g + 1];
           float v2 = acc[t][4 * g + 2], v3 = acc[t][4 * g + 3];
           if constexpr (TRAIN && l.mask >= 0) {
@@ -393,8 +494,9 @@ struct Chain {
             if constexpr (l.epi == EPI_RELU) { p0 = relu_bf16x2(p0); p1 = relu_bf16x2(p1); }
             BinT& b = bin[2 * t + (g >> 1)];
             if ((g & 1) == 0) { b[0] = p0; b[1] = p1; } else { b[2] = p0; b[3] = p1; }
-            if constexpr (TRAIN && l.plane >= 0)
-              plane_store_packed<E>(ry, voff, YF, wglob, t, g, u32x2{p0, p1});
+            pg[g] = u32x2{p0, p1};
+            if constexpr (plane_of(LI) && !defers(LI))
+              if (g & 1) plane_store_pair(ry, voff[4 + (g >> 1)], YF, wglob, t, pg[g - 1], pg[g]);
           } else {
             if constexpr (l.epi == EPI_RELU) {
               v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
@@ -439,6 +541,10 @@ struct Chain {
     }
   }
 
+  // bit of the mask word holding the sign of element (tile t, group g, i):
+  // the forward epilogue shifts them in with v_alignbit, oldest at bit 31
+  static constexpr int mask_pos(int t, int g, int i) { return 31 - ((t & 1) * 16 + 4 * g + i); }
+
   template <int LI>
   __device__ static void epilogue_bwd(const ChainArgs& a, BinT* bin, f32x16* acc, const float* prm,
                                       const char* smem, int h, int lane, int w, int m, int wglob,
@@ -452,19 +558,14 @@ struct Chain {
     const float* ws = prm + kWsOff + 4 * h;
 #pragma unroll
     for (int t = 0; t < l.T; ++t) {
+      u32x2 pg[4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int row0 = 32 * t + 8 * g + 4 * h;
         float v[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           v[i] = acc[t][4 * g + i];
-          if constexpr (l.epi == EPI_BMASK) {
-            // sign bit of the forward pre-activation: set -> ReLU was off
-            const int pos = 31 - ((t & 1) * 16 + 4 * g + i);
-            const uint32_t off = (uint32_t)__builtin_amdgcn_sbfe((int)mw[t >> 1], pos, 1);
-            v[i] = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, v[i]) & ~off);
-          }
+          if constexpr (l.epi == EPI_BMASK && !kBf16) v[i] = relu_mask(v[i], mw[t >> 1], mask_pos(t, g, i));
         }
         if constexpr (l.epi == EPI_BSIGMA) {
           const f32x4 w4 = *(const f32x4*)(ws + 32 * t + 8 * g);
@@ -472,10 +573,22 @@ struct Chain {
           for (int i = 0; i < 4; ++i) v[i] = fadd_rn(v[i], fmul_rn(ds, w4[i]));
         }
         if constexpr (kBf16) {
-          const uint32_t p0 = pack_bf16x2(v[0], v[1]), p1 = pack_bf16x2(v[2], v[3]);
+          uint32_t p0 = pack_bf16x2(v[0], v[1]), p1 = pack_bf16x2(v[2], v[3]);
+          if constexpr (l.epi == EPI_BMASK) {
+            static_for<0, 2>([&](auto gi) {
+              static_for<0, 4>([&](auto gg) {
+                if (gg == g && gi == (t & 1)) {
+                  p0 = relu_mask_bf16x2<mask_pos(gi, gg, 0), mask_pos(gi, gg, 1)>(p0, mw[t >> 1]);
+                  p1 = relu_mask_bf16x2<mask_pos(gi, gg, 2), mask_pos(gi, gg, 3)>(p1, mw[t >> 1]);
+                }
+              });
+            });
+          }
           BinT& b = bin[2 * t + (g >> 1)];
           if ((g & 1) == 0) { b[0] = p0; b[1] = p1; } else { b[2] = p0; b[3] = p1; }
-          plane_store_packed<E>(rdA, voff, width, wglob, t, g, u32x2{p0, p1});
+          pg[g] = u32x2{p0, p1};
+          if constexpr (!defers(LI))
+            if (g & 1) plane_store_pair(rdA, voff[4 + (g >> 1)], width, wglob, t, pg[g - 1], pg[g]);
         } else {
 #pragma unroll
           for (int i = 0; i < 4; ++i) bin[16 * t + 4 * g + i] = v[i];

@@ -159,22 +159,35 @@ inline constexpr int f32_acc_feature(int q, int h) {
 inline constexpr int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 // ---- activation planes in HBM: wave-tiled, bank-swizzled --------------------
-// A plane of width F (multiple of 32) over Mp samples is stored per 32-sample
-// wave tile w, per 32-feature tile t, per 8-feature group g as 64 "positions"
-// of 4 consecutive features (8 B bf16 / 16 B fp32).  The position of sample s
-// (0..31) and feature half hh = (f >> 2) & 1 is
+// A plane of width F (multiple of 32) over Mp samples is stored slab by slab:
+// a 32-sample slab is one contiguous run of F * 32 elements, made of 32-feature
+// tiles.  Inside a tile the layout depends on the element size.
+//
+// fp32 (16 B = 4 features): per 8-feature group g, 64 "positions" of 4
+// consecutive features; sample s, feature half hh = (f >> 2) & 1 sits at
 //     pos = ((s + 8 g + 4 hh) & 31) + 32 hh,
-// i.e. the lanes of one epilogue store instruction (lane = s + 32 h writes
-// features 32t + 8g + 4h .. +3) fill one contiguous 64 x 4-element block, and a
-// 32-sample x F slab is one contiguous F*32*es-byte run.  The rotation by
-// 8g + 4hh makes the transposed LDS reads of the dW kernel (4 samples x 4
-// features per lane, 32 lanes spanning 4 samples x 32 features) hit 64
-// distinct banks.
+// so one epilogue store instruction (lane = s + 32 h writes features
+// 32t + 8g + 4h .. +3) fills one contiguous 64 x 16 B block.
+//
+// bf16 (16 B = 8 features): per 16-feature pair block gp, 64 positions of 8
+// consecutive features 16 gp + 8 gg .. +7; sample s sits at
+//     pos = 32 gg + ((s + 8 gp + 4 gg) & 31).
+// The chain epilogues exchange lane halves (v_permlane32_swap) so that lane
+// s + 32 gg holds exactly those 8 features and one 16-B store per lane fills a
+// whole 1 KiB pair block.  The rotation by 8 gp + 4 gg makes the dW kernel's
+// transposed LDS reads (ds_read_b64_tr_b16: 4 samples x 4 features per lane,
+// a 32-lane half spanning 4 samples x 32 features) hit 64 distinct banks.
 inline constexpr int tile_pos(int s, int g, int hh) { return ((s + 8 * g + 4 * hh) & 31) + 32 * hh; }
-// byte offset of features f .. f+3 (f % 4 == 0) of sample m
+inline constexpr int bf16_pos(int s, int gp, int gg) { return 32 * gg + ((s + 8 * gp + 4 * gg) & 31); }
+// byte offset, inside a 32-sample slab, of features f .. f+3 (f % 4 == 0) of sample s
+inline constexpr int slab_off(int s, int f, int es) {
+  return es == 2 ? (f >> 5) * 2048 + ((f >> 4) & 1) * 1024 + bf16_pos(s, (f >> 4) & 1, (f >> 3) & 1) * 16 +
+                       ((f >> 2) & 1) * 8
+                 : (f >> 5) * 4096 + ((f >> 3) & 3) * 1024 + tile_pos(s, (f >> 3) & 3, (f >> 2) & 1) * 16;
+}
+// byte offset of features f .. f+3 of sample m in a plane of width F
 inline constexpr uint64_t plane_off(uint64_t m, int f, int F, int es) {
-  return (((m >> 5) * (uint64_t)(F >> 5) + (uint64_t)(f >> 5)) * 4 + (uint64_t)((f >> 3) & 3)) * (256u * es) +
-         (uint64_t)tile_pos((int)(m & 31), (f >> 3) & 3, (f >> 2) & 1) * (4u * es);
+  return (m >> 5) * (uint64_t)F * 32u * (uint64_t)es + (uint64_t)slab_off((int)(m & 31), f, es);
 }
 // prologue planes (PE, dir, drgb, sigma-head columns): the q-th value a lane
 // half h holds goes to column 8 (q / 4) + 4 h + (q % 4), so it is written by the

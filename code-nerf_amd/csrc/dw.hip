@@ -1,37 +1,28 @@
 // Weight gradients of the CodeNeRF MLP: dW_L = sum_m dA_L[m] (x) X_L[m].
 //
-// The reduction runs over samples (K = M ~ 1e6): a workgroup owns the WHOLE
-// (<= 256 x 288) gradient of one layer over one slice of the samples, so each
-// operand byte is read from HBM exactly once (this pass is HBM-bound: ~7.7 KB
-// of bf16 operands per sample against 0.9 MFLOP).  Every 32-sample slab of an
-// operand is one contiguous run in the wave-tiled plane layout (cn_layout.h);
-// it is staged through registers into a double-buffered LDS image that keeps
-// the HBM layout, and read back transposed:
-//   bf16: ds_read_b64_tr_b16 (4 samples x 1 feature per lane per read; the
-//         layout's rotation makes the reads bank-conflict free) feeding
-//         v_mfma_f32_32x32x16_bf16 with K = samples;
-//   fp32: ds_read_b32 feeding v_mfma_f32_32x32x2_f32 (exact fp32).
-// Bias gradients (row sums of dA) come from the A fragments; the sigma head
-// (ds x y_shape, 1 x 256) is a VALU side-product of the viewdir job.  Slices
-// write fp32 partials; dw_reduce sums them (deterministic, no atomics), maps
-// padded / permuted columns back to the reference tensors, adds the
-// code-injection correction db (x) z and accumulates into .grad.
+// The reduction runs over samples (K = M ~ 2e6): a persistent workgroup (one
+// per CU) owns the WHOLE (<= 288 x 288) gradient of one layer over one
+// byte-balanced slice of the (layer, slab) stream, so every operand byte is
+// read from HBM exactly once.  This pass is HBM-bound: 8,000 B of bf16
+// operands per sample against 0.9 MFLOP.  A 32-sample slab of a plane is one
+// contiguous run (cn_layout.h); it lands in LDS unchanged and is read back
+// transposed.
+//   bf16 (DwBf16<KIND>): one compile-time body per operand shape (DwKind),
+//     4-slot LDS-DMA ring (three slabs in flight while one is consumed),
+//     ds_read_b64_tr_b16 (conflict-free by the pair-block rotation) feeding
+//     v_mfma_f32_32x32x16_bf16; the sigma head (ds x y_shape) is an extra
+//     MFMA tile of the viewdir body;
+//   fp32 (DwF32): exact fp32 parity path, register-staged double buffer,
+//     ds_read_b32 + v_mfma_f32_32x32x2_f32.
+// Bias gradients (row sums of dA) come from the A fragments.  Workgroups write
+// fp32 partials; dw_reduce sums them (deterministic, no atomics), maps padded /
+// permuted columns back to the reference tensors, adds the code-injection
+// correction db (x) z and accumulates into .grad.
 #include "cn_common.h"
 #include "chain_args.h"
 #include "dw_args.h"
 
 namespace cn {
-
-template <int P>
-struct DwCfg;
-template <> struct DwCfg<CN_P_BF16> {
-  using E = __bf16;
-  static constexpr int kLoads = 5;      // 16-byte pieces per thread per slab (<= 18 x 2 KiB)
-};
-template <> struct DwCfg<CN_P_FP32> {
-  using E = float;
-  static constexpr int kLoads = 9;      // <= 18 x 4 KiB
-};
 
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -39,59 +30,45 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 template <int ES>
 CN_DEV int img_off(int s, int f) {
   // byte offset, inside a staged slab image, of features f..f+3 of sample s
-  return (f >> 5) * (1024 * ES) + ((f >> 3) & 3) * (256 * ES) + tile_pos(s, (f >> 3) & 3, (f >> 2) & 1) * (4 * ES);
+  return slab_off(s, f, ES);
 }
 
-// One segment: the slabs [t0, t1) of one problem, accumulated into a partial.
-template <int P>
-struct DwSeg {
-  using C = DwCfg<P>;
-  using E = typename C::E;
-  static constexpr bool kBf16 = P == CN_P_BF16;
-  static constexpr int ES = sizeof(E);
+// ------------------------------------------------------------ fp32 body
+// The exact-fp32 parity path: one generic body for every operand shape (the
+// shape is read from the problem at run time), slabs staged through
+// registers into a double-buffered LDS image, v_mfma_f32_32x32x2_f32 with
+// K = samples.  8 waves: wave w owns rows 64 (w >> 1) .. +63 and columns
+// 128 (w & 1) .. +127 (+ the 9th, dir-PE, column tile on the (w & 1) == 0
+// waves); the sigma head (ds x y_shape) is a VALU side product.
+struct DwF32 {
+  static constexpr int ES = 4;
   static constexpr int kTileB = 1024 * ES;                // one 32-sample x 32-feature tile
   static constexpr int kStage = 18 * kTileB;              // A (<= 9 tiles) + X (<= 9 tiles)
-#ifndef CN_DW_DEPTH
-#define CN_DW_DEPTH 2
-#endif
-  static constexpr int kDepth = CN_DW_DEPTH;              // bf16: slabs in flight
-  static constexpr int kG = 5;                            // 8 waves x 5 KiB = 40 KiB >= 36 KiB
-  static constexpr int kRingStage = 8 * kG * 1024;
-  static constexpr int kSmem = kBf16 ? (kDepth + 1) * kRingStage : 2 * kStage;
+  static constexpr int kLoads = 9;                        // 16-B pieces per thread per slab
+  static constexpr int kSmem = 2 * kStage;
 
-  // FULL: a 256 x 256 layer (8 out tiles, 8 X tiles, no sigma head) -- the
-  // bulk of the bytes; every wave is live and the loop is branch-free, so
-  // the LDS reads of a k-step can be issued ahead of its MFMAs.
-  template <bool FULL>
-  __device__ static void run(const DwProblem& pr, int t0, int t1, int rot, float* part, float* dbpart,
-                             char* smem) {
+  __device__ static void run(const DwProblem& pr, int t0, int t1, int rot, float* part, float* dbpart, char* smem) {
     const int nst = t1 - t0;
     // slab visited at step st: rotated so that the workgroups streaming one
-    // plane do not walk it in lockstep at a power-of-two stride (HBM channel
-    // camping); the sum does not depend on the order.
+    // plane do not walk it in lockstep (HBM channel camping); the sum does
+    // not depend on the order.
     rot %= nst;
     auto slab = [&](int st) { const int t = st + rot; return t0 + (t >= nst ? t - nst : t); };
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wo = w >> 1, wi = w & 1;           // rows 64*wo.., cols 128*wi..
+    const int wo = w >> 1, wi = w & 1;
     const int h = lane >> 5;
-    const int xt = pr.x0_tiles + pr.x1_tiles;    // staged X feature tiles
-    const bool extra = !FULL && (wi == 0) && xt > 8;   // 9th X tile (dir PE) on the wi == 0 waves
-    const int a_bytes = FULL ? 8 * kTileB : pr.a_tiles * kTileB;
-    const int x0_bytes = FULL ? 8 * kTileB : pr.x0_tiles * kTileB;
-    const int x1_bytes = FULL ? 0 : pr.x1_tiles * kTileB;
+    const int xt = pr.x0_tiles + pr.x1_tiles;
+    const bool extra = (wi == 0) && xt > 8;
+    const int a_bytes = pr.a_tiles * kTileB;
+    const int x0_bytes = pr.x0_tiles * kTileB;
+    const int x1_bytes = pr.x1_tiles * kTileB;
     const int stage_pieces = (a_bytes + x0_bytes + x1_bytes) >> 4;
-    const bool row0_live = FULL || 64 * wo < pr.out_tiles * 32;
-    const bool row1_live = FULL || 64 * wo + 32 < pr.out_tiles * 32;
-    const bool cols_live = FULL || 128 * wi < min(xt, 8) * 32;
-#if defined(CN_DW_NOCOMPUTE)
-    const bool live = false;   // A/B measurement only: pure streaming
-#elif defined(CN_DW_FULLONLY)
-    const bool live = FULL;    // A/B measurement only: no compute on the ragged problems
-#else
-    const bool live = FULL || (row0_live && (cols_live || extra));
-#endif
-    const bool sigma_head = !FULL && pr.sigma_head;
+    const bool row0_live = 64 * wo < pr.out_tiles * 32;
+    const bool row1_live = 64 * wo + 32 < pr.out_tiles * 32;
+    const bool cols_live = 128 * wi < min(xt, 8) * 32;
+    const bool live = row0_live && (cols_live || extra);
+    const bool sigma_head = pr.sigma_head;
 
     f32x16 acc[2][5];
 #pragma unroll
@@ -108,32 +85,12 @@ struct DwSeg {
       // byte b of the slab of wave tile `tile`: [A tiles | X0 tiles | X1 tiles]
       if (b < a_bytes) return pa0 + (size_t)tile * pr.a_width * 32 * ES + b;
       if (b < a_bytes + x0_bytes) return p00 + (size_t)tile * pr.x0_width * 32 * ES + (b - a_bytes);
-      if (b < a_bytes + x0_bytes + x1_bytes)
-        return p10 + (size_t)tile * pr.x1_width * 32 * ES + (b - a_bytes - x0_bytes);
-      return pa0;                                         // dummy piece
+      return p10 + (size_t)tile * pr.x1_width * 32 * ES + (b - a_bytes - x0_bytes);
     };
-    // bf16 staging: LDS-DMA ring, kDepth slabs in flight; every wave issues
-    // exactly kG 1-KiB pieces per slab (pieces past the slab re-read the
-    // first KiB into a dummy area) so one compile-time vmcnt fits all problems.
-    // The DMA is opaque to the compiler (glds16_opaque): the explicit vmcnt
-    // waits below are the only synchronisation.  The slab loop is unrolled by
-    // the ring size so every slot offset is a compile-time constant.
-    auto issue_dma = [&](int st, auto slotc) {
-      char* dst = smem + decltype(slotc)::value * kRingStage;
-#ifdef CN_DW_NOLOAD
-      if (st >= 0) return;       // A/B measurement only: compute on stale LDS
-#endif
-#pragma unroll
-      for (int k = 0; k < kG; ++k) {
-        const int piece = w * kG + k;
-        glds16_opaque(src_of(slab(st), piece * 1024) + lane * 16, lds_addr(dst + piece * 1024));
-      }
-    };
-    // fp32 staging (parity path): registers, double buffered
-    u32x4 rg[C::kLoads];
+    u32x4 rg[kLoads];
     auto gload = [&](int tile) {
 #pragma unroll
-      for (int k = 0; k < C::kLoads; ++k) {
+      for (int k = 0; k < kLoads; ++k) {
         const int b = (threadIdx.x + 512 * k) << 4;
         rg[k] = (threadIdx.x + 512 * k) < stage_pieces ? *(const u32x4*)src_of(tile, b) : u32x4{};
       }
@@ -141,89 +98,36 @@ struct DwSeg {
     auto lstore = [&](int buf) {
       char* dst = smem + buf * kStage;
 #pragma unroll
-      for (int k = 0; k < C::kLoads; ++k)
+      for (int k = 0; k < kLoads; ++k)
         if ((threadIdx.x + 512 * k) < stage_pieces) *(u32x4*)(dst + ((threadIdx.x + 512 * k) << 4)) = rg[k];
     };
 
-    if constexpr (kBf16) {
-      static_for<0, kDepth>([&](auto i) {
-        if (i < nst) issue_dma(i, i);
-      });
-    } else {
-      if (nst > 0) {
-        gload(slab(0));
-        lstore(0);
-      }
-      __syncthreads();
-    }
-    constexpr int kRing = kBf16 ? kDepth + 1 : 2;
-    auto body = [&](int st, auto slotc) {
-      constexpr int SL = decltype(slotc)::value;
-      const char* A;
-      if constexpr (kBf16) {
-        // slab st landed (own pieces), then every wave's pieces (barrier);
-        // the slot refilled below held slab st-1, which all waves finished.
-        const int ahead = min(kDepth - 1, nst - 1 - st);   // later slabs already issued
-        static_for<0, kDepth>([&](auto n) {
-          if (n == ahead) wait_vmcnt<n * kG>();
-        });
-        block_barrier();
-        if (st + kDepth < nst) issue_dma(st + kDepth, std::integral_constant<int, (SL + kDepth) % kRing>{});
-        A = smem + SL * kRingStage;
-      } else {
-        if (st + 1 < nst) gload(slab(st + 1));
-        A = smem + SL * kStage;
-      }
+    gload(slab(0));
+    lstore(0);
+    __syncthreads();
+    for (int st = 0; st < nst; ++st) {
+      if (st + 1 < nst) gload(slab(st + 1));
+      const char* A = smem + (st & 1) * kStage;
       const char* X = A + a_bytes;
       if (live) {
-        if constexpr (kBf16) {
-          const int G = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-#pragma unroll
-          for (int kk = 0; kk < 32; kk += 16) {
-            const int s = kk + 8 * h + q;
-            bf16x8 fa[2];
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-              const int f = 64 * wo + 32 * i + 16 * (G & 1) + 4 * p;
-              s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(A + img_off<ES>(s, f)));
-              s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(A + img_off<ES>(s + 4, f)));
-              fa[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-              float sum = 0.f;
-#pragma unroll
-              for (int j = 0; j < 8; ++j) sum += (float)fa[i][j];
-              dbacc[i] += sum;
-            }
-#pragma unroll
-            for (int j = 0; j < 5; ++j) {
-              if (j < 4 ? !cols_live : !extra) continue;
-              const int f = (j < 4 ? 128 * wi + 32 * j : 256) + 16 * (G & 1) + 4 * p;
-              s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(X + img_off<ES>(s, f)));
-              s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(X + img_off<ES>(s + 4, f)));
-              const bf16x8 fx = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-              acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fx, acc[0][j], 0, 0, 0);
-              if (row1_live) acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fx, acc[1][j], 0, 0, 0);
-            }
-          }
-        } else {
-          const int c = lane & 31;
+        const int c = lane & 31;
 #pragma unroll 4
-          for (int q = 0; q < 16; ++q) {
-            const int s = 2 * q + h;
-            float fa[2];
+        for (int q = 0; q < 16; ++q) {
+          const int s = 2 * q + h;
+          float fa[2];
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-              const int f = 64 * wo + 32 * i + c;
-              fa[i] = *(const float*)(A + img_off<ES>(s, f & ~3) + (f & 3) * 4);
-              dbacc[i] += fa[i];
-            }
+          for (int i = 0; i < 2; ++i) {
+            const int f = 64 * wo + 32 * i + c;
+            fa[i] = *(const float*)(A + img_off<ES>(s, f & ~3) + (f & 3) * 4);
+            dbacc[i] += fa[i];
+          }
 #pragma unroll
-            for (int j = 0; j < 5; ++j) {
-              if (j < 4 ? !cols_live : !extra) continue;
-              const int f = (j < 4 ? 128 * wi + 32 * j : 256) + c;
-              const float fx = *(const float*)(X + img_off<ES>(s, f & ~3) + (f & 3) * 4);
-              acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[0], fx, acc[0][j], 0, 0, 0);
-              if (row1_live) acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[1], fx, acc[1][j], 0, 0, 0);
-            }
+          for (int j = 0; j < 5; ++j) {
+            if (j < 4 ? !cols_live : !extra) continue;
+            const int f = (j < 4 ? 128 * wi + 32 * j : 256) + c;
+            const float fx = *(const float*)(X + img_off<ES>(s, f & ~3) + (f & 3) * 4);
+            acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[0], fx, acc[0][j], 0, 0, 0);
+            if (row1_live) acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[1], fx, acc[1][j], 0, 0, 0);
           }
         }
       }
@@ -233,23 +137,16 @@ struct DwSeg {
         const int s0 = (threadIdx.x >> 8) * 16;
 #pragma unroll 4
         for (int s = s0; s < s0 + 16; ++s) {
-          const E* dsp = (const E*)(A + img_off<ES>(s, 256));
-          const float ds = (float)dsp[0] + (float)dsp[1];
-          const float y = (float)((const E*)(X + img_off<ES>(s, f & ~3)))[f & 3];
+          const float* dsp = (const float*)(A + img_off<ES>(s, 256));
+          const float ds = dsp[0] + dsp[1];
+          const float y = ((const float*)(X + img_off<ES>(s, f & ~3)))[f & 3];
           sg = __builtin_fmaf(ds, y, sg);
           sgb += ds;
         }
       }
-      if constexpr (!kBf16) {
-        if (st + 1 < nst) lstore((st + 1) & 1);
-        __syncthreads();
-      }
-    };
-    for (int base = 0; base < nst; base += kRing)
-      static_for<0, kRing>([&](auto k) {
-        if (base + k < nst) body(base + k, k);
-      });
-    __syncthreads();
+      if (st + 1 < nst) lstore((st + 1) & 1);
+      __syncthreads();
+    }
 
     // ---- fp32 partial: row n (out feature), column c (in feature)
     if (live) {
@@ -486,7 +383,7 @@ struct DwBf16 {
 
 template <int P>
 __global__ __launch_bounds__(512, 2) void dw_kernel(DwArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[P == CN_P_BF16 ? kDwSmemBf16 : DwSeg<P>::kSmem];
+  __shared__ __attribute__((aligned(16))) char smem[P == CN_P_BF16 ? kDwSmemBf16 : DwF32::kSmem];
   const int g = blockIdx.x;
   const long long total = a.wprefix[a.nprob];
   const long long b0 = dw_share_begin(g, total, a.nwg), b1 = dw_share_begin(g + 1, total, a.nwg);
@@ -507,10 +404,8 @@ __global__ __launch_bounds__(512, 2) void dw_kernel(DwArgs a) {
         case DW_RGB0: DwBf16<DW_RGB0>::run(pr, t0, t1, g * 613, part, dbpart, smem); break;
         default: DwBf16<DW_RGB2>::run(pr, t0, t1, g * 613, part, dbpart, smem); break;
       }
-    } else if (pr.out_tiles == 8 && pr.a_tiles == 8 && pr.x0_tiles == 8 && pr.x1_tiles == 0 && !pr.sigma_head) {
-      DwSeg<P>::template run<true>(pr, t0, t1, g * 613, part, dbpart, smem);
     } else {
-      DwSeg<P>::template run<false>(pr, t0, t1, g * 613, part, dbpart, smem);
+      DwF32::run(pr, t0, t1, g * 613, part, dbpart, smem);
     }
     ++seg;
   }
@@ -582,7 +477,7 @@ __global__ __launch_bounds__(256) void dw_reduce_kernel(DwRedArgs a) {
 // ---------------------------------------------------------------- bias only
 template <int P>
 __global__ __launch_bounds__(256) void db_kernel(DbArgs a) {
-  using E = typename DwCfg<P>::E;
+  using E = std::conditional_t<P == CN_P_BF16, __bf16, float>;
   constexpr int ES = sizeof(E);
   const int j = blockIdx.y, blk = blockIdx.x, f = threadIdx.x;
   const int s0 = blk * a.slabs_per_blk, s1 = min(a.total_slabs, s0 + a.slabs_per_blk);

@@ -48,14 +48,21 @@ def act_offsets(Mp, es):
 
 
 def decode(act, off, F, Mp, dtype):
-    """(Mp, F) float64 view of a wave-tiled plane (plane_off, csrc/cn_layout.h)."""
+    """(Mp, F) float64 view of a wave-tiled plane (slab_off, csrc/cn_layout.h)."""
     es = torch.finfo(dtype).bits // 8
     dev = act.device
     m = torch.arange(Mp, device=dev)[:, None]
     f = torch.arange(F, device=dev)[None, :]
-    g, hh, s = (f >> 3) & 3, (f >> 2) & 1, m & 31
-    pos = ((s + 8 * g + 4 * hh) & 31) + 32 * hh
-    elem = ((((m >> 5) * (F >> 5) + (f >> 5)) * 4 + g) * 256 + pos * 4 + (f & 3))
+    s = m & 31
+    slab = (m >> 5) * (F * 32) + (f >> 5) * 1024
+    if es == 2:     # 16-feature pair blocks of 64 x 8 elements
+        gp, gg = (f >> 4) & 1, (f >> 3) & 1
+        pos = 32 * gg + ((s + 8 * gp + 4 * gg) & 31)
+        elem = slab + gp * 512 + pos * 8 + (f & 7)
+    else:           # 8-feature groups of 64 x 4 elements
+        g, hh = (f >> 3) & 3, (f >> 2) & 1
+        pos = ((s + 8 * g + 4 * hh) & 31) + 32 * hh
+        elem = slab + g * 256 + pos * 4 + (f & 3)
     flat = act[off:off + Mp * F * es].view(dtype)
     return flat[elem].double()
 

@@ -94,6 +94,12 @@ def main():
         y = torch.empty_like(x)
         t = timeit(lambda: y.copy_(x), 10)
         out["copy_GBs"] = round(2 * x.numel() / t / 1e6, 1)
+        xf = x.view(torch.float32)
+        t = timeit(lambda: xf.fill_(1.0), 10)
+        out["fill_GBs"] = round(x.numel() / t / 1e6, 1)
+        acc = torch.empty(1, device=dev)
+        t = timeit(lambda: torch.sum(xf, dim=0, out=acc), 10)
+        out["read_GBs"] = round(x.numel() / t / 1e6, 1)
     out["lib"] = os.environ.get("CODENERF_LIB", "default")
     print(json.dumps(out))
 
