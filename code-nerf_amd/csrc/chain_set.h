@@ -171,6 +171,23 @@ int dw_setup(char* act, int M, const float* zvec, float* dbuf, char* ws, DwArgs*
   const long long nwg = kDwWorkgroups;
   if ((wsum + min_total - 1) / min_total >= nwg) return -1;
   dw->nwg = red->nwg = (int)nwg;
+  // which partial slots hold each problem (the kernel's own segment walk)
+  for (int L = 0; L < N::kFwdLayers; ++L) red->gfirst[L] = -1;
+  for (int g = 0; g < (int)nwg; ++g) {
+    const long long b0 = dw_share_begin(g, wsum, (int)nwg), b1 = dw_share_begin(g + 1, wsum, (int)nwg);
+    int seg = 0;
+    for (int L = 0; L < N::kFwdLayers && seg < 2; ++L) {
+      int t0, t1;
+      dw_slab_range(dw->wprefix, dw->pbytes, dw->total_tiles, L, b0, b1, t0, t1);
+      if (t1 <= t0) continue;
+      if (red->gfirst[L] < 0) { red->gfirst[L] = g; red->gseg[L] = seg; }
+      else if (seg != 0) return -1;      // only a problem's first workgroup may hold it second
+      red->glast[L] = g;
+      ++seg;
+    }
+  }
+  for (int L = 0; L < N::kFwdLayers; ++L)
+    if (red->gfirst[L] < 0) return -1;
   dw->part = (float*)ws;
   dw->dbpart = (float*)(ws + (size_t)kDwWorkgroups * 2 * kPartRows * kPartCols * sizeof(float));
   red->part = dw->part;

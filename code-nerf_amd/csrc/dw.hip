@@ -201,11 +201,11 @@ template <> struct DwShape<DW_VIEWDIR> { static constexpr int kA = 9, kX0 = 8, k
 template <> struct DwShape<DW_RGB0>    { static constexpr int kA = 4, kX0 = 8, kX1 = 0, NI = 2, NJ = 2; };
 template <> struct DwShape<DW_RGB2>    { static constexpr int kA = 1, kX0 = 4, kX1 = 0, NI = 1, NJ = 1; };
 
-constexpr int kDwSlot = 36 * 1024;        // largest stage (viewdir: 18 tiles x 2 KiB)
-constexpr int kDwRing = 4;
-constexpr int kDwDepth = kDwRing - 1;     // slabs in flight while one is consumed
-constexpr int kDwDummy = kDwRing * kDwSlot;   // landing area of padding pieces (<= 6 KiB)
-constexpr int kDwSmemBf16 = kDwDummy + 8 * 1024;
+// LDS ring per shape: 256x256 slabs (32 KiB stages, no padding pieces) and
+// the other shapes (36 KiB = the viewdir stage, + an 8 KiB landing area for
+// padding pieces) both keep 4 slots, 3 slabs in flight: a 5-slot ring for the
+// 256x256 bodies measured 0.2 ms slower per C2 step.
+constexpr int kDwSmemBf16 = 160 * 1024;
 
 template <int KIND>
 struct DwBf16 {
@@ -214,7 +214,15 @@ struct DwBf16 {
   static constexpr int kPieces = 2 * (kA + kX0 + kX1);     // 1 KiB pieces per slab
   static constexpr int kG = (kPieces + 7) / 8;              // pieces per wave per slab
   static constexpr bool kVD = KIND == DW_VIEWDIR;
-  static_assert(kPieces * 1024 <= kDwSlot && (8 * kG - kPieces) * 1024 <= 8 * 1024, "dw stage");
+#ifndef CN_DW_RING_FULL
+#define CN_DW_RING_FULL 4
+#endif
+  static constexpr int kDwSlot = KIND == DW_FULL ? 32 * 1024 : 36 * 1024;
+  static constexpr int kDwRing = KIND == DW_FULL ? CN_DW_RING_FULL : 4;
+  static constexpr int kDwDepth = kDwRing - 1;        // slabs in flight while one is consumed
+  static constexpr int kDwDummy = kDwRing * kDwSlot;  // landing area of padding pieces
+  static_assert(kPieces * 1024 <= kDwSlot, "dw stage");
+  static_assert(kDwDummy + (8 * kG - kPieces) * 1024 <= kDwSmemBf16, "dw LDS");
 
   // wave w's row tile i / column tile j (wave-uniform)
   static CN_DEV int row_tile(int w, int i) {
@@ -423,34 +431,11 @@ __global__ __launch_bounds__(256) void dw_reduce_kernel(DwRedArgs a) {
   const DwRedProblem& p = a.p[pi];
   const int e = gid - a.prefix[pi];
   const int n = e / p.cols, c = e % p.cols;
-  // workgroups whose share holds slabs of problem pi (contiguous range)
-  const long long total = a.wprefix[a.nprob];
-  int g_lo = (int)(a.wprefix[pi] * a.nwg / (total > 0 ? total : 1)) - 1;
-  int g_hi = (int)(a.wprefix[pi + 1] * a.nwg / (total > 0 ? total : 1)) + 1;
-  g_lo = max(0, g_lo);
-  g_hi = min(a.nwg - 1, g_hi);
   float v = 0.f, db = 0.f;
   const bool need_db = (c == 0) || p.z;
-  for (int g = g_lo; g <= g_hi; ++g) {
-    const long long b0 = dw_share_begin(g, total, a.nwg), b1 = dw_share_begin(g + 1, total, a.nwg);
-    // does g own slabs of pi?  (start byte of pi's slab t is wprefix + t*pb)
-    const long long lo = max(b0, a.wprefix[pi]), hi = min(b1, a.wprefix[pi + 1]);
-    if (hi <= lo) continue;
-    // a slab start inside [lo, hi)?
-    const long long pb = p.pbytes;
-    const long long first = ((lo - a.wprefix[pi]) + pb - 1) / pb * pb + a.wprefix[pi];
-    if (first >= hi) continue;
-    // segment index: 1 if the previous problem also has slabs in g
-    int seg = 0;
-    if (pi > 0) {
-      const long long lo2 = max(b0, a.wprefix[pi - 1]), hi2 = min(b1, a.wprefix[pi]);
-      if (hi2 > lo2) {
-        const long long pb2 = a.p[pi - 1].pbytes;
-        const long long f2 = ((lo2 - a.wprefix[pi - 1]) + pb2 - 1) / pb2 * pb2 + a.wprefix[pi - 1];
-        if (f2 < hi2) seg = 1;
-      }
-    }
-    const size_t slot = (size_t)g * 2 + seg;
+  const int gf = a.gfirst[pi], gl = a.glast[pi];
+  for (int g = gf; g <= gl; ++g) {
+    const size_t slot = (size_t)g * 2 + (g == gf ? a.gseg[pi] : 0);
     v += a.part[slot * kPartRows * kPartCols + (size_t)n * kPartCols + c];
     if (need_db) db += a.dbpart[slot * kPartRows + n];
   }

@@ -89,6 +89,9 @@ struct DwRedArgs {
   long long wprefix[kDwMaxProblems + 1];
   const float* part;            // DwArgs::part
   const float* dbpart;
+  // workgroups holding slabs of problem p: gfirst[p] .. glast[p]; the first
+  // one may hold it as its second segment (gseg[p]), the others as their first
+  int gfirst[kDwMaxProblems], glast[kDwMaxProblems], gseg[kDwMaxProblems];
 };
 
 // Bias gradients of the layers that follow a code injection only (codes-only
