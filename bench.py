@@ -45,6 +45,9 @@ def parse():
     ap.add_argument("--objects", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    # rehearsal of the N > 1 path on a one-GPU box: gloo, every rank on cuda:0
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--one-device", action="store_true")
     return ap.parse_args()
 
 
@@ -92,12 +95,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.one_device:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)     # RCCL over xGMI
+        else:
+            dist.init_process_group("gloo")
 
     from codenerf_amd.model import CodeNeRF
     from codenerf_amd.trainer_core import TrainCore
