@@ -43,6 +43,11 @@ def parse():
     ap.add_argument("--n-fine", type=int, default=64)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--objects", type=int, default=64)
+    # other BASELINE configs, measured for DESIGN.md (the driver runs c2):
+    #   c4: optimize.py test-time code optimisation, 50 views x 128^2 x 64
+    #       samples per step, fwd + dX only (no weight gradients), bf16
+    #   c5: 256^2, 128 + 128 samples, fp32, the image in 8 ray parts
+    ap.add_argument("--config", default="c2", choices=["c2", "c4", "c5"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     # rehearsal of the N > 1 path on a one-GPU box: gloo, every rank on cuda:0
@@ -87,11 +92,20 @@ class Timers:
         self.ev.setdefault(name, []).append((s, e))
 
     def summary(self):
-        return {k: sum(s.elapsed_time(e) for s, e in v) / len(v) for k, v in self.ev.items()}
+        """phase -> (mean ms per launch, total ms over the timed steps)"""
+        out = {}
+        for k, v in self.ev.items():
+            tot = sum(s.elapsed_time(e) for s, e in v)
+            out[k] = (tot / len(v), tot)
+        return out
 
 
 def main():
     args = parse()
+    if args.config == "c4":
+        args.H, args.n_coarse, args.n_fine, args.precision = 128, 64, 0, "bf16"
+    elif args.config == "c5":
+        args.H, args.n_coarse, args.n_fine, args.precision = 256, 128, 128, "fp32"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -133,10 +147,34 @@ def main():
     poses = [make_pose(1.3, float(torch.rand(1, generator=g)) * 360 - 180,
                        float(torch.rand(1, generator=g)) * 50 - 10).to(dev) for _ in range(n_views)]
 
+    ray_parts = 8 if args.config == "c5" else 1
+    views_per_step = 50 if args.config == "c4" else 1
+    if args.config == "c4":
+        # src/optimizer.py:66-98: codes only (weights fixed), every target view
+        # accumulates into the code gradients, then one AdamW step on the codes
+        from codenerf_amd.optim import FusedAdamW
+        from codenerf_amd.render import ImageStep
+        from codenerf_amd import engine as _eng
+        img = ImageStep(model, chunk=2048, reg_coef=1e-4, timers=timers)
+        sc1 = torch.nn.Parameter(shape_codes.detach()[:1].clone())
+        tc1 = torch.nn.Parameter(texture_codes.detach()[:1].clone())
+        copt = FusedAdamW([{"params": [sc1], "lr": 1e-2}, {"params": [tc1], "lr": 1e-2}])
+        poses += [make_pose(1.3, float(torch.rand(1, generator=g)) * 360 - 180,
+                            float(torch.rand(1, generator=g)) * 50 - 10).to(dev) for _ in range(50 - n_views)]
+        gts += [gts[k % n_views] for k in range(50 - n_views)]
+
     def step(i):
+        if args.config == "c4":
+            sc1.grad = torch.zeros_like(sc1)
+            tc1.grad = torch.zeros_like(tc1)
+            for v in range(views_per_step):
+                ro, vd = _eng.get_rays_dev(H, W, focal, True, poses[v])
+                img.forward_backward(ro, vd, core.stratified_z(dev), gts[v], sc1, tc1, 0, weight_grads=False)
+            copt.step()
+            return
         v = i % n_views
         obj = object_for(i, rank, world, n_obj)
-        core.train_step(H, W, focal, poses[v], gts[v], obj)
+        core.train_step(H, W, focal, poses[v], gts[v], obj, ray_parts=ray_parts)
 
     for i in range(args.warmup):
         step(i)
@@ -157,30 +195,36 @@ def main():
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    samples_per_step = R * (args.n_coarse + args.n_fine)
+    samples_per_step = R * (args.n_coarse + args.n_fine) * views_per_step
     value = samples_per_step * world * args.steps / dt
     ms = dt / args.steps * 1e3
 
-    kern = timers.summary()
+    summ = timers.summary()
+    kern = {k: v[0] for k, v in summ.items()}                     # ms per launch
+    per_step = {k: v[1] / args.steps for k, v in summ.items()}    # ms per step (all launches)
     peak = BF16_PEAK_TFLOPS if args.precision == "bf16" else FP32_PEAK_TFLOPS
     roof = None
     if kern:
         flops = {k: FLOP_PER_SAMPLE[k] * samples_per_step for k in FLOP_PER_SAMPLE if k in kern}
-        dom = max(flops, key=lambda k: kern[k])
-        achieved = flops[dom] / (kern[dom] * 1e-3) / 1e12
+        if args.config == "c4":
+            flops.pop("dw", None)       # codes-only: the dw timer brackets the bias sums
+        dom = max(flops, key=lambda k: per_step[k])
+        # algorithmic FLOPs of the phase per step / its launch time per step
+        achieved = flops[dom] / (per_step[dom] * 1e-3) / 1e12
         roof = {"bound": "mfma", "kernel": {"fwd": "chain_kernel<fwd,train>", "bwd": "chain_kernel<bwd>",
                                             "dw": "dw_kernel"}[dom],
                 "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": load_traffic(dom),
-                "ms_per_launch": {k: round(v, 4) for k, v in kern.items()}}
+                "ms_per_launch": {k: round(v, 4) for k, v in kern.items()},
+                "ms_per_step_by_phase": {k: round(v, 4) for k, v in per_step.items()}}
         if dom == "dw" and args.precision == "bf16":
             # the weight-gradient pass streams the stored bf16 operands (dA and X
             # planes, 8,000 B per sample at the srncar net): its practical limiter
             dw_bytes = DW_BYTES_PER_SAMPLE * samples_per_step
-            gbs = dw_bytes / (kern["dw"] * 1e-3) / 1e9
+            gbs = dw_bytes / (per_step["dw"] * 1e-3) / 1e9
             roof["hbm_view"] = {"bytes_per_launch": dw_bytes, "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
                                 "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
-        step_flops = sum(FLOP_PER_SAMPLE.values()) * samples_per_step
+        step_flops = sum(v for k, v in FLOP_PER_SAMPLE.items() if args.config != "c4" or k != "dw") * samples_per_step
         roof["step"] = {"achieved": round(step_flops / (ms * 1e-3) / 1e12, 2), "unit": "TFLOP/s",
                         "frac": round(step_flops / (ms * 1e-3) / 1e12 / peak, 4)}
 
@@ -189,14 +233,19 @@ def main():
         cpu = cpu_baseline(args.cpu_threads)
 
     if rank == 0:
+        metric = {"c2": "ray-samples/sec (train step), SRN-cars 128x128, 64 coarse + 64 fine samples",
+                  "c4": "ray-samples/sec (optimize.py code optimisation step), 50 views x 128x128 x 64 samples",
+                  "c5": "ray-samples/sec (train step), SRN-cars 256x256, 128 coarse + 128 fine samples, fp32"}
         out = {
-            "metric": "ray-samples/sec (train step), SRN-cars 128x128, 64 coarse + 64 fine samples",
+            "metric": metric[args.config],
             "value": round(value, 1), "unit": "ray-samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
-            "data": "synthetic (random 128x128 targets, poses on a radius-1.3 sphere, random-init weights)",
+            "data": f"synthetic (random {H}x{W} targets, poses on a radius-1.3 sphere, random-init weights)",
             "config": {"workload": f"srncar.json net, {H}x{W} image/object/step, {args.n_coarse}+{args.n_fine} "
-                                   f"samples/ray, train step incl. AdamW", "objects_per_step": world,
+                                   f"samples/ray, " + ("50 views, codes-only fwd+dX+AdamW" if args.config == "c4"
+                                                       else "train step incl. AdamW"),
+                       "name": args.config, "objects_per_step": world,
                        "rays_per_step_per_gpu": R, "parallelism": f"dp{world}"},
             "roofline": roof,
             "cpu_baseline": cpu,

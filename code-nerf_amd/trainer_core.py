@@ -39,19 +39,37 @@ class TrainCore:
         z = torch.linspace(self.near + half, self.far - half, n, device=device)
         return z + torch.rand(n, device=device) * (self.far - self.near) / (2 * n)
 
-    def train_step(self, H, W, focal, c2w, gt, obj):
+    def train_step(self, H, W, focal, c2w, gt, obj, ray_parts=1):
+        """ray_parts > 1 renders the image as that many contiguous ray ranges
+        (each a multiple of the loss chunk, so the chunk-mean semantics are
+        unchanged; the regulariser is counted once, on the first part) whose
+        gradients accumulate before the one AdamW step: bounds the activation
+        workspace for large images (C5: 256^2 x 256 samples in fp32)."""
         dev = c2w.device
         ro, vd = _eng.get_rays_dev(H, W, focal, True, c2w)
         z = self.stratified_z(dev)
         self.bucket.zero()
-        if self.n_fine:
-            rand_f = torch.rand(H * W, self.n_fine, device=dev)
-            loss_c, loss_f, rgb, reg = self.step_impl.forward_backward_fine(
-                ro, vd, z, rand_f, gt, self.shape_codes, self.texture_codes, obj)
-            losses = (loss_c, loss_f)
-        else:
-            losses, rgb, reg = self.step_impl.forward_backward(ro, vd, z, gt, self.shape_codes,
-                                                               self.texture_codes, obj)
+        R = H * W
+        if R % ray_parts or (R // ray_parts) % self.step_impl.chunk:
+            raise ValueError("ray_parts must split the image into whole loss chunks")
+        P = R // ray_parts
+        rand_f = torch.rand(R, self.n_fine, device=dev) if self.n_fine else None
+        losses, rgbs = [], []
+        for k in range(ray_parts):
+            sl = slice(k * P, (k + 1) * P)
+            if self.n_fine:
+                loss_c, loss_f, rgb, _ = self.step_impl.forward_backward_fine(
+                    ro[sl], vd[sl], z, rand_f[sl], gt[sl], self.shape_codes, self.texture_codes, obj, reg=k == 0)
+                losses.append((loss_c, loss_f))
+            else:
+                loss, rgb, _ = self.step_impl.forward_backward(ro[sl], vd[sl], z, gt[sl], self.shape_codes,
+                                                              self.texture_codes, obj, reg=k == 0)
+                losses.append(loss)
+            rgbs.append(rgb)
         self.bucket.all_reduce(self.dist)
         self.opt.step()
-        return losses, rgb
+        if ray_parts == 1:
+            return losses[0], rgbs[0]
+        if self.n_fine:
+            return (torch.cat([l[0] for l in losses]), torch.cat([l[1] for l in losses])), torch.cat(rgbs)
+        return torch.cat(losses), torch.cat(rgbs)
