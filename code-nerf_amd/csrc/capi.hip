@@ -226,9 +226,9 @@ int cn_latent_bwd(const cn_plan* p, const float* const* d_params, float* const* 
   if (!p || !d_params || !d_grads || !d_shape || !d_tex || !d_zvec || !d_dbuf || !d_scratch || !d_dshape || !d_dtex)
     return fail("cn_latent_bwd: NULL argument");
   LatentBwdArgs a{d_params, d_grads, d_shape, d_tex, d_zvec, d_dbuf, d_scratch, d_dshape, d_dtex, reg_coef, d_reg_out};
-  hipLaunchKernelGGL(p->cs.latent_bwd, dim3(p->cs.n_inject), dim3(256), 0, S(stream), a);
+  hipLaunchKernelGGL(p->cs.latent_bwd, dim3(p->cs.n_inject, kLatentRowBlocks), dim3(256), 0, S(stream), a);
   if (launch_check("latent_bwd_kernel")) return -1;
-  hipLaunchKernelGGL(p->cs.code_grad, dim3(2), dim3(256), 0, S(stream), a);
+  hipLaunchKernelGGL(p->cs.code_grad, dim3(2), dim3(1024), 0, S(stream), a);
   return launch_check("code_grad_kernel");
 }
 

@@ -59,7 +59,12 @@ __global__ __launch_bounds__(256) void latent_bwd_kernel(LatentBwdArgs a) {
   constexpr ParamIdx P{SB, TB};
   __shared__ float db[256];
   __shared__ float dp[256];
+  // grid (kInject, kLatentRowBlocks): block (j, r) recomputes dz_j (a GEMV
+  // over W_j, L2-resident) and updates rows [32 r, 32 r + 32) of d L_j, so the
+  // 256 KB read-modify-write of each latent weight gradient is spread over
+  // kLatentRowBlocks workgroups; block r == 0 also writes dpre and d c_j
   const int j = blockIdx.x;
+  const int rb = blockIdx.y;
   const int i = threadIdx.x;
   const bool shape = j < SB;
   const int wl = shape ? P.shape_w(j) : P.tex_w(j - SB);          // layer fed by z_j
@@ -72,38 +77,50 @@ __global__ __launch_bounds__(256) void latent_bwd_kernel(LatentBwdArgs a) {
   for (int n = 0; n < 256; ++n) dz = __builtin_fmaf(W[(size_t)n * 256 + i], db[n], dz);
   const float d = a.zvec[j * 256 + i] > 0.f ? dz : 0.f;
   dp[i] = d;
-  a.dpre[j * 256 + i] = d;
-  a.grads[lw + 1][i] += d;
+  if (rb == 0) {
+    a.dpre[j * 256 + i] = d;
+    a.grads[lw + 1][i] += d;
+  }
   __syncthreads();
   const float* code = shape ? a.shape_code : a.texture_code;
   const float ck = code[i];
   float* gL = a.grads[lw];
-  for (int r = 0; r < 256; ++r) gL[(size_t)r * 256 + i] += dp[r] * ck;
+  constexpr int kRows = 256 / kLatentRowBlocks;
+#pragma unroll 8
+  for (int r = rb * kRows; r < (rb + 1) * kRows; ++r) gL[(size_t)r * 256 + i] += dp[r] * ck;
 }
 
 template <int SB, int TB>
-__global__ __launch_bounds__(256) void code_grad_kernel(LatentBwdArgs a) {
+__global__ __launch_bounds__(1024) void code_grad_kernel(LatentBwdArgs a) {
+  // 4 groups of 256 threads each take a quarter of the rows i of every L_j;
+  // their partial sums are added in a fixed order (deterministic)
   constexpr ParamIdx P{SB, TB};
   __shared__ float red[256];
+  __shared__ float part[4][256];
   const bool shape = blockIdx.x == 0;
-  const int k = threadIdx.x;
+  const int k = threadIdx.x & 255, q = threadIdx.x >> 8;
   const float* code = shape ? a.shape_code : a.texture_code;
   const int j0 = shape ? 0 : SB, j1 = shape ? SB : SB + TB;
-  float g = 0.f;
+  float gq = 0.f;
   for (int j = j0; j < j1; ++j) {
     const int lw = shape ? P.shape_latent_w(j) : P.tex_latent_w(j - SB);
     const float* L = a.params[lw];
     const float* d = a.dpre + j * 256;
-    for (int i = 0; i < 256; ++i) g = __builtin_fmaf(L[(size_t)i * 256 + k], d[i], g);
+#pragma unroll 8
+    for (int i = 64 * q; i < 64 * q + 64; ++i) gq = __builtin_fmaf(L[(size_t)i * 256 + k], d[i], gq);
   }
-  // regulariser reg_coef * mean(|s| + |t|) over the (1, 256) codes
+  part[q][k] = gq;
+  // regulariser reg_coef * mean(|s| + |t|) over the (1, 256) codes; every
+  // thread of the block passes every barrier, group 0 does the work
   const float c = code[k];
-  red[k] = c * c;
+  if (q == 0) red[k] = c * c;
   __syncthreads();
   for (int s = 128; s > 0; s >>= 1) {
-    if (k < s) red[k] += red[k + s];
+    if (q == 0 && k < s) red[k] += red[k + s];
     __syncthreads();
   }
+  if (q != 0) return;
+  float g = (part[0][k] + part[1][k]) + (part[2][k] + part[3][k]);
   const float nrm = sqrtf(red[0]);
   if (a.reg_coef != 0.f && nrm > 0.f) g += a.reg_coef * (c / nrm);
   (shape ? a.d_shape_code : a.d_texture_code)[k] += g;

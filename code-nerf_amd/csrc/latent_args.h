@@ -3,6 +3,8 @@
 
 namespace cn {
 
+constexpr int kLatentRowBlocks = 8;   // workgroups per latent weight-gradient update (latent_bwd_kernel)
+
 struct LatentArgs {
   const float* const* params;   // device array of the reference parameters
   const float* shape_code;      // [256]
