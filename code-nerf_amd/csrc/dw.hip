@@ -33,166 +33,13 @@ CN_DEV int img_off(int s, int f) {
   return slab_off(s, f, ES);
 }
 
-// ------------------------------------------------------------ fp32 body
-// The exact-fp32 parity path: one generic body for every operand shape (the
-// shape is read from the problem at run time), slabs staged through
-// registers into a double-buffered LDS image, v_mfma_f32_32x32x2_f32 with
-// K = samples.  8 waves: wave w owns rows 64 (w >> 1) .. +63 and columns
-// 128 (w & 1) .. +127 (+ the 9th, dir-PE, column tile on the (w & 1) == 0
-// waves); the sigma head (ds x y_shape) is a VALU side product.
-struct DwF32 {
-  static constexpr int ES = 4;
-  static constexpr int kTileB = 1024 * ES;                // one 32-sample x 32-feature tile
-  static constexpr int kStage = 18 * kTileB;              // A (<= 9 tiles) + X (<= 9 tiles)
-  static constexpr int kLoads = 9;                        // 16-B pieces per thread per slab
-  static constexpr int kSmem = 2 * kStage;
-
-  __device__ static void run(const DwProblem& pr, int t0, int t1, int rot, float* part, float* dbpart, char* smem) {
-    const int nst = t1 - t0;
-    // slab visited at step st: rotated so that the workgroups streaming one
-    // plane do not walk it in lockstep (HBM channel camping); the sum does
-    // not depend on the order.
-    rot %= nst;
-    auto slab = [&](int st) { const int t = st + rot; return t0 + (t >= nst ? t - nst : t); };
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wo = w >> 1, wi = w & 1;
-    const int h = lane >> 5;
-    const int xt = pr.x0_tiles + pr.x1_tiles;
-    const bool extra = (wi == 0) && xt > 8;
-    const int a_bytes = pr.a_tiles * kTileB;
-    const int x0_bytes = pr.x0_tiles * kTileB;
-    const int x1_bytes = pr.x1_tiles * kTileB;
-    const int stage_pieces = (a_bytes + x0_bytes + x1_bytes) >> 4;
-    const bool row0_live = 64 * wo < pr.out_tiles * 32;
-    const bool row1_live = 64 * wo + 32 < pr.out_tiles * 32;
-    const bool cols_live = 128 * wi < min(xt, 8) * 32;
-    const bool live = row0_live && (cols_live || extra);
-    const bool sigma_head = pr.sigma_head;
-
-    f32x16 acc[2][5];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 5; ++j) acc[i][j] = f32x16{};
-    float dbacc[2] = {0.f, 0.f};
-    float sg = 0.f, sgb = 0.f;                   // sigma head: ds x y (feature tid & 255), sum ds
-
-    const char* pa0 = (const char*)pr.A;
-    const char* p00 = (const char*)pr.X0;
-    const char* p10 = pr.X1 ? (const char*)pr.X1 : p00;
-    auto src_of = [&](int tile, int b) -> const char* {
-      // byte b of the slab of wave tile `tile`: [A tiles | X0 tiles | X1 tiles]
-      if (b < a_bytes) return pa0 + (size_t)tile * pr.a_width * 32 * ES + b;
-      if (b < a_bytes + x0_bytes) return p00 + (size_t)tile * pr.x0_width * 32 * ES + (b - a_bytes);
-      return p10 + (size_t)tile * pr.x1_width * 32 * ES + (b - a_bytes - x0_bytes);
-    };
-    u32x4 rg[kLoads];
-    auto gload = [&](int tile) {
-#pragma unroll
-      for (int k = 0; k < kLoads; ++k) {
-        const int b = (threadIdx.x + 512 * k) << 4;
-        rg[k] = (threadIdx.x + 512 * k) < stage_pieces ? *(const u32x4*)src_of(tile, b) : u32x4{};
-      }
-    };
-    auto lstore = [&](int buf) {
-      char* dst = smem + buf * kStage;
-#pragma unroll
-      for (int k = 0; k < kLoads; ++k)
-        if ((threadIdx.x + 512 * k) < stage_pieces) *(u32x4*)(dst + ((threadIdx.x + 512 * k) << 4)) = rg[k];
-    };
-
-    gload(slab(0));
-    lstore(0);
-    __syncthreads();
-    for (int st = 0; st < nst; ++st) {
-      if (st + 1 < nst) gload(slab(st + 1));
-      const char* A = smem + (st & 1) * kStage;
-      const char* X = A + a_bytes;
-      if (live) {
-        const int c = lane & 31;
-#pragma unroll 4
-        for (int q = 0; q < 16; ++q) {
-          const int s = 2 * q + h;
-          float fa[2];
-#pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            const int f = 64 * wo + 32 * i + c;
-            fa[i] = *(const float*)(A + img_off<ES>(s, f & ~3) + (f & 3) * 4);
-            dbacc[i] += fa[i];
-          }
-#pragma unroll
-          for (int j = 0; j < 5; ++j) {
-            if (j < 4 ? !cols_live : !extra) continue;
-            const int f = (j < 4 ? 128 * wi + 32 * j : 256) + c;
-            const float fx = *(const float*)(X + img_off<ES>(s, f & ~3) + (f & 3) * 4);
-            acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[0], fx, acc[0][j], 0, 0, 0);
-            if (row1_live) acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[1], fx, acc[1][j], 0, 0, 0);
-          }
-        }
-      }
-      if (sigma_head) {
-        // d w_sigma[f] += sum_s ds[s] * y[s][f];  ds = A[s][256] + A[s][257]
-        const int f = threadIdx.x & 255;
-        const int s0 = (threadIdx.x >> 8) * 16;
-#pragma unroll 4
-        for (int s = s0; s < s0 + 16; ++s) {
-          const float* dsp = (const float*)(A + img_off<ES>(s, 256));
-          const float ds = dsp[0] + dsp[1];
-          const float y = ((const float*)(X + img_off<ES>(s, f & ~3)))[f & 3];
-          sg = __builtin_fmaf(ds, y, sg);
-          sgb += ds;
-        }
-      }
-      if (st + 1 < nst) lstore((st + 1) & 1);
-      __syncthreads();
-    }
-
-    // ---- fp32 partial: row n (out feature), column c (in feature)
-    if (live) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        if (i == 1 && !row1_live) continue;
-#pragma unroll
-        for (int j = 0; j < 5; ++j) {
-          if (j < 4 ? !cols_live : !extra) continue;
-          const int col = (j < 4 ? 128 * wi + 32 * j : 256) + (lane & 31);
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int row = 64 * wo + 32 * i + acc_row(r, h);
-            part[(size_t)row * kPartCols + col] = acc[i][j][r];
-          }
-        }
-      }
-    }
-    if (wi == 0) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const float tot = dbacc[i] + __shfl_xor(dbacc[i], 32);
-        const bool rl = i == 0 ? row0_live : row1_live;
-        if (h == 0 && rl) dbpart[64 * wo + 32 * i + (lane & 31)] = tot;
-      }
-    }
-    if (sigma_head) {
-      // combine the two sample halves through LDS (the staging buffers are free now)
-      float* red = (float*)smem;
-      red[threadIdx.x] = sg;
-      red[512 + threadIdx.x] = sgb;
-      __syncthreads();
-      if (threadIdx.x < 256) {
-        part[(size_t)256 * kPartCols + threadIdx.x] = red[threadIdx.x] + red[threadIdx.x + 256];
-        if (threadIdx.x == 0) dbpart[256] = red[512] + red[512 + 256];
-      }
-    }
-    __syncthreads();
-  }
-};
-
-// ------------------------------------------------------------ bf16 bodies
-// One compile-time body per operand shape (DwKind): every wave's tiles, LDS
-// reads, MFMAs and piece counts are constants, so the slab loop has no
-// runtime branches beyond wave-uniform role tests.  Staging: a 4-slot LDS-DMA
-// ring of 36 KiB slots, three slabs in flight while the fourth is consumed.
+// ------------------------------------------------------------ bodies
+// One compile-time body per (precision, operand shape): every wave's tiles,
+// LDS reads, MFMAs and piece counts are constants, so the slab loop has no
+// runtime branches beyond wave-uniform role tests.  Staging by LDS-DMA:
+//   bf16: 4-slot ring of 32 / 36 KiB slots, three slabs in flight;
+//   fp32: 2-slot ring of 72 KiB slots, one slab in flight (this path is
+//         MFMA-bound: 16 K SIMD cycles of v_mfma_f32_32x32x2_f32 per slab).
 template <int KIND> struct DwShape;
 //                                      A tiles, X0, X1, row tiles/wave, col tiles/wave
 template <> struct DwShape<DW_FULL>    { static constexpr int kA = 8, kX0 = 8, kX1 = 0, NI = 2, NJ = 4; };
@@ -205,24 +52,25 @@ template <> struct DwShape<DW_RGB2>    { static constexpr int kA = 1, kX0 = 4, k
 // the other shapes (36 KiB = the viewdir stage, + an 8 KiB landing area for
 // padding pieces) both keep 4 slots, 3 slabs in flight: a 5-slot ring for the
 // 256x256 bodies measured 0.2 ms slower per C2 step.
-constexpr int kDwSmemBf16 = 160 * 1024;
+constexpr int kDwSmem = 160 * 1024;
 
-template <int KIND>
-struct DwBf16 {
+template <int P, int KIND>
+struct DwBody {
   using Sh = DwShape<KIND>;
+  static constexpr bool kBf16 = P == CN_P_BF16;
+  static constexpr int ES = kBf16 ? 2 : 4;
+  static constexpr int TB = 1024 * ES;                      // one 32-sample x 32-feature tile
   static constexpr int kA = Sh::kA, kX0 = Sh::kX0, kX1 = Sh::kX1, NI = Sh::NI, NJ = Sh::NJ;
-  static constexpr int kPieces = 2 * (kA + kX0 + kX1);     // 1 KiB pieces per slab
+  static constexpr int kPA = kA * TB / 1024, kPX0 = kX0 * TB / 1024;   // 1 KiB pieces of A / X0
+  static constexpr int kPieces = (kA + kX0 + kX1) * TB / 1024;       // 1 KiB pieces per slab
   static constexpr int kG = (kPieces + 7) / 8;              // pieces per wave per slab
   static constexpr bool kVD = KIND == DW_VIEWDIR;
-#ifndef CN_DW_RING_FULL
-#define CN_DW_RING_FULL 4
-#endif
-  static constexpr int kDwSlot = KIND == DW_FULL ? 32 * 1024 : 36 * 1024;
-  static constexpr int kDwRing = KIND == DW_FULL ? CN_DW_RING_FULL : 4;
+  static constexpr int kDwSlot = kBf16 ? (KIND == DW_FULL ? 32 * 1024 : 36 * 1024) : 72 * 1024;
+  static constexpr int kDwRing = kBf16 ? 4 : 2;
   static constexpr int kDwDepth = kDwRing - 1;        // slabs in flight while one is consumed
   static constexpr int kDwDummy = kDwRing * kDwSlot;  // landing area of padding pieces
   static_assert(kPieces * 1024 <= kDwSlot, "dw stage");
-  static_assert(kDwDummy + (8 * kG - kPieces) * 1024 <= kDwSmemBf16, "dw LDS");
+  static_assert(kDwDummy + (8 * kG - kPieces) * 1024 <= kDwSmem, "dw LDS");
 
   // wave w's row tile i / column tile j (wave-uniform)
   static CN_DEV int row_tile(int w, int i) {
@@ -277,11 +125,11 @@ struct DwBf16 {
         const int piece = w * kG + k;            // wave-uniform
         const char* src;
         uint32_t dst = lds_addr(smem + decltype(slotc)::value * kDwSlot + piece * 1024);
-        if (piece < 2 * kA) src = pa + t * (kA * 2048) + piece * 1024;
-        else if (piece < 2 * (kA + kX0)) src = px0 + t * (kX0 * 2048) + (piece - 2 * kA) * 1024;
-        else if (piece < kPieces) src = px1 + t * (kX1 * 2048) + (piece - 2 * (kA + kX0)) * 1024;
+        if (piece < kPA) src = pa + t * (kA * TB) + piece * 1024;
+        else if (piece < kPA + kPX0) src = px0 + t * (kX0 * TB) + (piece - kPA) * 1024;
+        else if (piece < kPieces) src = px1 + t * (kX1 * TB) + (piece - kPA - kPX0) * 1024;
         else {
-          src = pa + t * (kA * 2048);            // padding piece: re-read, never consumed
+          src = pa + t * (kA * TB);              // padding piece: re-read, never consumed
           dst = lds_addr(smem + kDwDummy + (piece - kPieces) * 1024);
         }
         glds16_opaque(src + lane * 16, dst);
@@ -314,8 +162,47 @@ struct DwBf16 {
       block_barrier();
       if (st + kDwDepth < nst) issue(st + kDwDepth, std::integral_constant<int, (SL + kDwDepth) % kDwRing>{});
       const char* A = smem + SL * kDwSlot;
-      const char* X = A + kA * 2048;
+      const char* X = A + kA * TB;
       if (!live) return;
+      if constexpr (!kBf16) {
+        // exact fp32: K = 2 samples per MFMA; lane l reads feature l & 31 of
+        // sample 2 qq + (l >> 5) (A: rows = out features, B: cols = inputs)
+        const int c = lane & 31;
+        auto val = [&](const char* base, int tile, int s) {
+          const int f = 32 * tile + c;
+          return *(const float*)(base + img_off<4>(s, f & ~3) + (f & 3) * 4);
+        };
+#pragma unroll 4
+        for (int qq = 0; qq < 16; ++qq) {
+          const int s = 2 * qq + h;
+          float fa[NI];
+#pragma unroll
+          for (int i = 0; i < NI; ++i) {
+            fa[i] = val(A, row_tile(w, i), s);
+            if (do_db) dbacc[i] += fa[i];
+          }
+          float fs = 0.f;
+          if constexpr (kVD) {
+            fs = val(A, 8, s);
+            if (w == 0) dbsig += fs;
+          }
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            const float fx = val(X, col_tile(w, j), s);
+#pragma unroll
+            for (int i = 0; i < NI; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i], fx, acc[i][j], 0, 0, 0);
+            if constexpr (kVD) {
+              if (j == (w >> 1)) acc_e2 = __builtin_amdgcn_mfma_f32_32x32x2f32(fs, fx, acc_e2, 0, 0, 0);
+            }
+          }
+          if constexpr (kVD) {
+            const float fd = val(X, 8, s);
+            const float fr = (w & 1) ? fa[1] : fa[0];
+            acc_e1 = __builtin_amdgcn_mfma_f32_32x32x2f32(fr, fd, acc_e1, 0, 0, 0);
+          }
+        }
+        return;
+      }
 #pragma unroll
       for (int kk = 0; kk < 32; kk += 16) {
         const int s = kk + 8 * h + q;
@@ -391,7 +278,7 @@ struct DwBf16 {
 
 template <int P>
 __global__ __launch_bounds__(512, 2) void dw_kernel(DwArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[P == CN_P_BF16 ? kDwSmemBf16 : DwF32::kSmem];
+  __shared__ __attribute__((aligned(16))) char smem[kDwSmem];
   const int g = blockIdx.x;
   const long long total = a.wprefix[a.nprob];
   const long long b0 = dw_share_begin(g, total, a.nwg), b1 = dw_share_begin(g + 1, total, a.nwg);
@@ -404,16 +291,12 @@ __global__ __launch_bounds__(512, 2) void dw_kernel(DwArgs a) {
     const DwProblem& pr = a.p[p];
     float* part = a.part + slot * kPartRows * kPartCols;
     float* dbpart = a.dbpart + slot * kPartRows;
-    if constexpr (P == CN_P_BF16) {
-      switch (pr.kind) {
-        case DW_FULL: DwBf16<DW_FULL>::run(pr, t0, t1, g * 613, part, dbpart, smem); break;
-        case DW_PE: DwBf16<DW_PE>::run(pr, t0, t1, g * 613, part, dbpart, smem); break;
-        case DW_VIEWDIR: DwBf16<DW_VIEWDIR>::run(pr, t0, t1, g * 613, part, dbpart, smem); break;
-        case DW_RGB0: DwBf16<DW_RGB0>::run(pr, t0, t1, g * 613, part, dbpart, smem); break;
-        default: DwBf16<DW_RGB2>::run(pr, t0, t1, g * 613, part, dbpart, smem); break;
-      }
-    } else {
-      DwF32::run(pr, t0, t1, g * 613, part, dbpart, smem);
+    switch (pr.kind) {
+      case DW_FULL: DwBody<P, DW_FULL>::run(pr, t0, t1, g * 613, part, dbpart, smem); break;
+      case DW_PE: DwBody<P, DW_PE>::run(pr, t0, t1, g * 613, part, dbpart, smem); break;
+      case DW_VIEWDIR: DwBody<P, DW_VIEWDIR>::run(pr, t0, t1, g * 613, part, dbpart, smem); break;
+      case DW_RGB0: DwBody<P, DW_RGB0>::run(pr, t0, t1, g * 613, part, dbpart, smem); break;
+      default: DwBody<P, DW_RGB2>::run(pr, t0, t1, g * 613, part, dbpart, smem); break;
     }
     ++seg;
   }
