@@ -49,6 +49,8 @@ _SIGS = {
     "cn_latent_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P]),
     "cn_mlp_fwd": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _I, _I, _P]),
     "cn_mlp_bwd": (_I, [_P, _P, _P, _I, _P, _P, _P, _P]),
+    "cn_mlp_fwd_codes": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _I, _I, _P]),
+    "cn_mlp_bwd_codes": (_I, [_P, _P, _P, _I, _P, _P, _P, _P]),
     "cn_mlp_dw": (_I, [_P, _P, _I, _P, _P, _P, _P, _P]),
     "cn_mlp_dbias": (_I, [_P, _P, _I, _P, _P, _P]),
     "cn_latent_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P]),

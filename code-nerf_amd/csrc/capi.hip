@@ -110,10 +110,11 @@ int cn_latent_fwd(const cn_plan* p, const float* const* d_params, const float* d
   return launch_check("latent_fwd_kernel");
 }
 
-int cn_mlp_fwd(const cn_plan* p, const void* d_pack, const float* d_blob, int M, const float* d_xyz,
-               const float* d_viewdir, const float* d_rays_o, const float* d_rays_d, const float* d_z,
-               int z_stride, int n_samples, float* d_sigma, float* d_rgb, void* d_act, int act_M, int act_row0,
-               void* stream) {
+static int mlp_fwd_impl(int codes, const cn_plan* p, const void* d_pack, const float* d_blob, int M,
+                        const float* d_xyz, const float* d_viewdir, const float* d_rays_o, const float* d_rays_d,
+                        const float* d_z, int z_stride, int n_samples, float* d_sigma, float* d_rgb, void* d_act,
+                        int act_M, int act_row0, void* stream) {
+  if (codes && !d_act) return fail("cn_mlp_fwd_codes: the activation workspace is required");
   if (!p || !d_pack || !d_blob || !d_sigma || !d_rgb) return fail("cn_mlp_fwd: NULL argument");
   if (M <= 0) return fail("cn_mlp_fwd: M must be positive");
   ChainArgs a{};
@@ -163,13 +164,29 @@ int cn_mlp_fwd(const cn_plan* p, const void* d_pack, const float* d_blob, int M,
     a.masks = (uint32_t*)(b + L.masks + (r0 / 32) * L.mask_bytes_per_slab);
   }
   const int grid = Mp / p->cs.tile;
-  hipLaunchKernelGGL(d_act ? p->cs.fwd_train : p->cs.fwd_infer, dim3(grid), dim3(p->cs.waves * 64), 0,
-                     S(stream), a);
+  hipLaunchKernelGGL(d_act ? (codes ? p->cs.fwd_codes : p->cs.fwd_train) : p->cs.fwd_infer, dim3(grid),
+                     dim3(p->cs.waves * 64), 0, S(stream), a);
   return launch_check("chain_kernel(fwd)");
 }
 
-int cn_mlp_bwd(const cn_plan* p, const void* d_pack, const float* d_blob, int M, const float* d_dsigma,
-               const float* d_drgb, void* d_act, void* stream) {
+int cn_mlp_fwd(const cn_plan* p, const void* d_pack, const float* d_blob, int M, const float* d_xyz,
+               const float* d_viewdir, const float* d_rays_o, const float* d_rays_d, const float* d_z,
+               int z_stride, int n_samples, float* d_sigma, float* d_rgb, void* d_act, int act_M, int act_row0,
+               void* stream) {
+  return mlp_fwd_impl(0, p, d_pack, d_blob, M, d_xyz, d_viewdir, d_rays_o, d_rays_d, d_z, z_stride, n_samples,
+                      d_sigma, d_rgb, d_act, act_M, act_row0, stream);
+}
+
+int cn_mlp_fwd_codes(const cn_plan* p, const void* d_pack, const float* d_blob, int M, const float* d_xyz,
+                     const float* d_viewdir, const float* d_rays_o, const float* d_rays_d, const float* d_z,
+                     int z_stride, int n_samples, float* d_sigma, float* d_rgb, void* d_act, int act_M,
+                     int act_row0, void* stream) {
+  return mlp_fwd_impl(1, p, d_pack, d_blob, M, d_xyz, d_viewdir, d_rays_o, d_rays_d, d_z, z_stride, n_samples,
+                      d_sigma, d_rgb, d_act, act_M, act_row0, stream);
+}
+
+static int mlp_bwd_impl(int codes, const cn_plan* p, const void* d_pack, const float* d_blob, int M,
+                        const float* d_dsigma, const float* d_drgb, void* d_act, void* stream) {
   if (!p || !d_pack || !d_blob || !d_dsigma || !d_drgb || !d_act) return fail("cn_mlp_bwd: NULL argument");
   if (M <= 0) return fail("cn_mlp_bwd: M must be positive");
   ChainArgs a{};
@@ -187,8 +204,19 @@ int cn_mlp_bwd(const cn_plan* p, const void* d_pack, const float* d_blob, int M,
   a.d8 = b + L.d8;
   a.spre = (float*)(b + L.spre);
   a.masks = (uint32_t*)(b + L.masks);
-  hipLaunchKernelGGL(p->cs.bwd, dim3(Mp / p->cs.tile), dim3(p->cs.waves * 64), 0, S(stream), a);
+  hipLaunchKernelGGL(codes ? p->cs.bwd_codes : p->cs.bwd, dim3(Mp / p->cs.tile), dim3(p->cs.waves * 64), 0,
+                     S(stream), a);
   return launch_check("chain_kernel(bwd)");
+}
+
+int cn_mlp_bwd(const cn_plan* p, const void* d_pack, const float* d_blob, int M, const float* d_dsigma,
+               const float* d_drgb, void* d_act, void* stream) {
+  return mlp_bwd_impl(0, p, d_pack, d_blob, M, d_dsigma, d_drgb, d_act, stream);
+}
+
+int cn_mlp_bwd_codes(const cn_plan* p, const void* d_pack, const float* d_blob, int M, const float* d_dsigma,
+                     const float* d_drgb, void* d_act, void* stream) {
+  return mlp_bwd_impl(1, p, d_pack, d_blob, M, d_dsigma, d_drgb, d_act, stream);
 }
 
 int cn_mlp_dw(const cn_plan* p, void* d_act, int M, const float* d_zvec, float* const* d_grads, float* d_dbuf,
@@ -211,7 +239,7 @@ int cn_mlp_dbias(const cn_plan* p, void* d_act, int M, float* d_dbuf, void* d_ws
   if (!p || !d_act || !d_dbuf || !d_ws) return fail("cn_mlp_dbias: NULL argument");
   if (M <= 0) return fail("cn_mlp_dbias: M must be positive");
   DbArgs db;
-  p->cs.db_setup((char*)d_act, M, d_dbuf, (char*)d_ws, &db);
+  if (p->cs.db_setup((char*)d_act, M, d_dbuf, (char*)d_ws, &db) < 0) return fail("cn_mlp_dbias: unsupported plane width");
   if (db.ninj <= 0) return 0;
   if (p->cs.prec) hipLaunchKernelGGL(db_kernel<CN_P_BF16>, dim3(kDbBlocks, db.ninj), dim3(256), 0, S(stream), db);
   else hipLaunchKernelGGL(db_kernel<CN_P_FP32>, dim3(kDbBlocks, db.ninj), dim3(256), 0, S(stream), db);

@@ -110,7 +110,7 @@ CN_DEV void plane_store_pair(__amdgpu_buffer_rsrc_t r, uint32_t voff16, int F, i
   asm volatile("s_nop 1" ::"v"(d) : "memory");
 }
 
-template <int P, int SB, int TB, bool BWD, int WAVES, bool TRAIN>
+template <int P, int SB, int TB, bool BWD, int WAVES, int MODE>
 struct Chain {
   using S = Sched<P, SB, TB, BWD>;
   using N = Net<SB, TB>;
@@ -118,6 +118,8 @@ struct Chain {
   using BinT = typename PT<P>::BinT;
   static constexpr int kBin = PT<P>::kBin;
   static constexpr bool kBf16 = (P == CN_P_BF16);
+  static constexpr bool TRAIN = MODE != CN_MODE_INFER;    // masks + sigma pre-activation
+  static constexpr bool PLANES = MODE == CN_MODE_TRAIN;   // every operand plane of dW
   static constexpr int NL = S::NL;
   static constexpr int kChunks = S::kChunks;
   static constexpr int G = kChunkBlocks / WAVES;   // LDS-DMA instructions per wave per chunk
@@ -154,7 +156,10 @@ struct Chain {
   // queue at the same time).  Store j of layer li-1 follows block
   // first_block(li) + j * lblocks(li) / n.  The last layer's plane (backward:
   // dA of the first forward layer) has no next layer and is stored in place.
-  static constexpr bool plane_of(int i) { return BWD ? true : (TRAIN && S::L(i).plane >= 0); }
+  static constexpr bool codes_plane(int p) { return MODE == CN_MODE_CODES && p >= 1 && N::fwd(p - 1).inj >= 0; }
+  static constexpr bool plane_of(int i) {
+    return BWD ? (PLANES || codes_plane(S::L(i).plane)) : (PLANES && S::L(i).plane >= 0);
+  }
   static constexpr bool defers(int i) { return kBf16 && plane_of(i) && i + 1 < NL; }
   static constexpr int deferred_count(int i) { return defers(i) ? 2 * S::L(i).T : 0; }
   // index j of the deferred store of layer li-1 issued after block g, or -1
@@ -180,7 +185,7 @@ struct Chain {
       if (l.epi == EPI_SHAPE) s += TRAIN ? 2 : 1;
       return s;   // EPI_RGB stores come after the last wait: not counted (safe)
     }
-    return defers(i) ? 0 : l.T * (kBf16 ? 2 : 4);
+    return plane_of(i) && !defers(i) ? l.T * (kBf16 ? 2 : 4) : 0;
   }
   static constexpr int stores_in_chunk(int c) {
     int s = 0;
@@ -392,7 +397,7 @@ struct Chain {
       for (int q = 0; q < 4; ++q)
         ((f32x4*)stash)[q] = f32x4{dp[4 * q], dp[4 * q + 1], dp[4 * q + 2], dp[4 * q + 3]};
     }
-    if constexpr (TRAIN) {
+    if constexpr (PLANES) {
       // slot q of lane half h -> column slot_col(h, q): group k = q / 4 lands in
       // feature tile k / 4, group k % 4 (cn_layout.h)
       const auto rp = mkrsrc(a.pe);
@@ -426,7 +431,7 @@ struct Chain {
       bin[0] = h ? g1 : g0;
       bin[1] = h ? 0.f : g2;
     }
-    {
+    if constexpr (PLANES) {
       // drgb as a padded 32-wide plane for the rgb-head weight gradient
       // (columns slot_col(0, 0..2) = 0..2)
       const auto r8 = mkrsrc(a.d8);
@@ -505,7 +510,7 @@ struct Chain {
             bin[16 * t + 4 * g + 1] = v1;
             bin[16 * t + 4 * g + 2] = v2;
             bin[16 * t + 4 * g + 3] = v3;
-            if constexpr (TRAIN && l.plane >= 0)
+            if constexpr (plane_of(LI))
               plane_store<E>(ry, voff, YF, wglob, t, g, v0, v1, v2, v3);
           }
         }
@@ -587,12 +592,12 @@ struct Chain {
           BinT& b = bin[2 * t + (g >> 1)];
           if ((g & 1) == 0) { b[0] = p0; b[1] = p1; } else { b[2] = p0; b[3] = p1; }
           pg[g] = u32x2{p0, p1};
-          if constexpr (!defers(LI))
+          if constexpr (plane_of(LI) && !defers(LI))
             if (g & 1) plane_store_pair(rdA, voff[4 + (g >> 1)], width, wglob, t, pg[g - 1], pg[g]);
         } else {
 #pragma unroll
           for (int i = 0; i < 4; ++i) bin[16 * t + 4 * g + i] = v[i];
-          plane_store<E>(rdA, voff, width, wglob, t, g, v[0], v[1], v[2], v[3]);
+          if constexpr (plane_of(LI)) plane_store<E>(rdA, voff, width, wglob, t, g, v[0], v[1], v[2], v[3]);
         }
       }
       acc[t] = f32x16{};
@@ -600,9 +605,9 @@ struct Chain {
   }
 };
 
-template <int P, int SB, int TB, bool BWD, int WAVES, bool TRAIN>
+template <int P, int SB, int TB, bool BWD, int WAVES, int MODE>
 __global__ __launch_bounds__(WAVES * 64, WAVES / 4) void chain_kernel(ChainArgs a) {
-  Chain<P, SB, TB, BWD, WAVES, TRAIN>::run(a);
+  Chain<P, SB, TB, BWD, WAVES, MODE>::run(a);
 }
 
 }  // namespace cn

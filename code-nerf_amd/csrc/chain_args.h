@@ -7,6 +7,15 @@ namespace cn {
 
 constexpr int kMaxPlanes = 12;
 
+// What a chain launch stores (template parameter MODE of chain_kernel).
+enum ChainMode : int {
+  CN_MODE_INFER = 0,   // outputs only
+  CN_MODE_TRAIN = 1,   // + every plane the backward and the dW pass read
+  CN_MODE_CODES = 2,   // codes-only optimisation (src/optimizer.py): forward stores
+                       // ReLU masks + sigma pre-activations, backward only the dA
+                       // planes of the layers fed by a code (the bias sums need them)
+};
+
 // Per-call bias blob (written by the latent kernel, read by the forward chain):
 //   [kFwdLayers][256]  bias of every forward layer (code injection folded in)
 //   [256]              sigma head weight (ws)

@@ -30,6 +30,8 @@ struct ChainSet {
   void (*fwd_train)(ChainArgs) = nullptr;
   void (*fwd_infer)(ChainArgs) = nullptr;
   void (*bwd)(ChainArgs) = nullptr;
+  void (*fwd_codes)(ChainArgs) = nullptr;   // codes-only optimisation (CN_MODE_CODES)
+  void (*bwd_codes)(ChainArgs) = nullptr;
   void (*latent_fwd)(LatentArgs) = nullptr;
   void (*latent_bwd)(LatentBwdArgs) = nullptr;
   void (*code_grad)(LatentBwdArgs) = nullptr;
@@ -41,7 +43,7 @@ struct ChainSet {
                   DwRedArgs* red) = nullptr;
   size_t (*dw_ws_bytes)(int M) = nullptr;
   // fills the bias-only argument block (dbuf rows of the injection layers)
-  void (*db_setup)(char* act, int M, float* dbuf, char* ws, DbArgs* db) = nullptr;
+  int (*db_setup)(char* act, int M, float* dbuf, char* ws, DbArgs* db) = nullptr;
 };
 
 ChainSet chain_set_fp32_3_1();

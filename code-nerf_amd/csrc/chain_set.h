@@ -196,7 +196,7 @@ int dw_setup(char* act, int M, const float* zvec, float* dbuf, char* ws, DwArgs*
 }
 
 template <int P, int SB, int TB>
-void db_setup(char* act, int M, float* dbuf, char* ws, DbArgs* db) {
+int db_setup(char* act, int M, float* dbuf, char* ws, DbArgs* db) {
   using N = Net<SB, TB>;
   const int Mp = ((M + 255) / 256) * 256;
   const ActLayout A = act_layout<P, SB, TB>(Mp);
@@ -210,11 +210,13 @@ void db_setup(char* act, int M, float* dbuf, char* ws, DbArgs* db) {
     if (inj < 0) continue;
     db->A[inj] = act + A.dA[L];
     db->a_width[inj] = N::dplane_width(L);
+    if (db->a_width[inj] != 256) return -1;     // db_kernel streams 256-wide planes
     ++n;
   }
   db->ninj = n;
   db->part = (float*)ws;
   db->dbout = dbuf;
+  return n;
 }
 
 template <int P, int SB, int TB>
@@ -233,9 +235,11 @@ ChainSet make_chain_set() {
   s.pack_fwd_bytes = Sched<P, SB, TB, false>::packed_bytes();
   s.pack_bwd_bytes = Sched<P, SB, TB, true>::packed_bytes();
   s.blob_floats = BiasBlob<SB, TB>::kFloats;
-  s.fwd_train = chain_kernel<P, SB, TB, false, WAVES, true>;
-  s.fwd_infer = chain_kernel<P, SB, TB, false, WAVES, false>;
-  s.bwd = chain_kernel<P, SB, TB, true, WAVES, true>;
+  s.fwd_train = chain_kernel<P, SB, TB, false, WAVES, CN_MODE_TRAIN>;
+  s.fwd_infer = chain_kernel<P, SB, TB, false, WAVES, CN_MODE_INFER>;
+  s.fwd_codes = chain_kernel<P, SB, TB, false, WAVES, CN_MODE_CODES>;
+  s.bwd = chain_kernel<P, SB, TB, true, WAVES, CN_MODE_TRAIN>;
+  s.bwd_codes = chain_kernel<P, SB, TB, true, WAVES, CN_MODE_CODES>;
   s.latent_fwd = latent_fwd_kernel<SB, TB>;
   s.latent_bwd = latent_bwd_kernel<SB, TB>;
   s.code_grad = code_grad_kernel<SB, TB>;

@@ -343,22 +343,61 @@ __global__ __launch_bounds__(256) void dw_reduce_kernel(DwRedArgs a) {
 }
 
 // ---------------------------------------------------------------- bias only
+// Column sums of the 256-wide dA planes of the code-fed layers, streamed in
+// 16-B chunks: in a slab, thread t reads chunks t + 256 k, which always hold
+// the same sample's 8 (bf16) / 4 (fp32) consecutive features of tiles
+// advancing with k; each lane sums its sample over the workgroup's slabs, then
+// the 32 lanes of a half-wave (the 32 samples) are combined by an xor tree.
 template <int P>
 __global__ __launch_bounds__(256) void db_kernel(DbArgs a) {
-  using E = std::conditional_t<P == CN_P_BF16, __bf16, float>;
-  constexpr int ES = sizeof(E);
-  const int j = blockIdx.y, blk = blockIdx.x, f = threadIdx.x;
+  constexpr bool kBf16 = P == CN_P_BF16;
+  constexpr int EPC = kBf16 ? 8 : 4;                // elements per 16-B chunk
+  constexpr int NK = 256 * (kBf16 ? 2 : 4) / 128;   // chunks per thread per slab (256-wide plane)
+  const int j = blockIdx.y, blk = blockIdx.x, t = threadIdx.x, lane = t & 63;
   const int s0 = blk * a.slabs_per_blk, s1 = min(a.total_slabs, s0 + a.slabs_per_blk);
-  const char* A = (const char*)a.A[j];
-  const size_t slab_bytes = (size_t)a.a_width[j] * 32 * ES;
-  const int foff = f & ~3, fe = (f & 3) * ES;
-  float sum = 0.f;
-  for (int t = s0; t < s1; ++t) {
-    const char* base = A + (size_t)t * slab_bytes + fe;
-#pragma unroll 8
-    for (int s = 0; s < 32; ++s) sum += (float)*(const E*)(base + img_off<ES>(s, foff));
+  const u32x4* A = (const u32x4*)a.A[j];
+  float acc[NK][EPC];
+#pragma unroll
+  for (int k = 0; k < NK; ++k)
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) acc[k][e] = 0.f;
+  for (int sl = s0; sl < s1; ++sl) {
+    const u32x4* base = A + (size_t)sl * (256 * NK) + t;
+    u32x4 v[NK];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) v[k] = base[256 * k];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      if constexpr (kBf16) {
+        const bf16x8 x = __builtin_bit_cast(bf16x8, v[k]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[k][e] += (float)x[e];
+      } else {
+        const f32x4 x = __builtin_bit_cast(f32x4, v[k]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[k][e] += x[e];
+      }
+    }
   }
-  a.part[((size_t)j * kDbBlocks + blk) * 256 + f] = sum;
+#pragma unroll
+  for (int k = 0; k < NK; ++k)
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) {
+      float x = acc[k][e];
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) x += __shfl_xor(x, o);
+      acc[k][e] = x;
+    }
+  if ((lane & 31) == 0) {
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const int c = t + 256 * k;
+      const int f0 = kBf16 ? 32 * (c >> 7) + 16 * ((c >> 6) & 1) + 8 * ((c >> 5) & 1)
+                           : 32 * (c >> 8) + 8 * ((c >> 6) & 3) + 4 * ((c >> 5) & 1);
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) a.part[((size_t)j * kDbBlocks + blk) * 256 + f0 + e] = acc[k][e];
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void db_reduce_kernel(DbArgs a) {

@@ -97,26 +97,30 @@ class Engine:
 
     # ------------------------------------------------------------ MLP
     def mlp_fwd(self, blob, M, xyz=None, viewdir=None, rays_o=None, rays_d=None, z=None, z_stride=0,
-                n_samples=0, act=None, act_M=0, act_row0=0, sigma=None, rgb=None):
+                n_samples=0, act=None, act_M=0, act_row0=0, sigma=None, rgb=None, codes=False):
         """act_M / act_row0: the workspace is sized for act_M samples and this
-        pass fills rows [act_row0, act_row0 + pad(M)) (coarse + fine passes)."""
+        pass fills rows [act_row0, act_row0 + pad(M)) (coarse + fine passes).
+        codes: codes-only optimisation -- store only what mlp_bwd(codes=True)
+        needs (cn_mlp_fwd_codes)."""
         Mp = self.pad(M)
         if sigma is None:
             sigma = torch.empty(Mp, dtype=torch.float32, device=self.device)
         if rgb is None:
             rgb = torch.empty(Mp, 3, dtype=torch.float32, device=self.device)
         assert sigma.numel() >= Mp and rgb.numel() >= 3 * Mp
-        check(self.L.cn_mlp_fwd(self._plan, ptr(self.pack_fwd), ptr(blob), M, ptr(xyz), ptr(viewdir),
-                                ptr(rays_o), ptr(rays_d), ptr(z), z_stride, n_samples, ptr(sigma), ptr(rgb),
-                                ptr(act), int(act_M), int(act_row0), self.stream), "cn_mlp_fwd")
+        fn = self.L.cn_mlp_fwd_codes if codes else self.L.cn_mlp_fwd
+        check(fn(self._plan, ptr(self.pack_fwd), ptr(blob), M, ptr(xyz), ptr(viewdir),
+                 ptr(rays_o), ptr(rays_d), ptr(z), z_stride, n_samples, ptr(sigma), ptr(rgb),
+                 ptr(act), int(act_M), int(act_row0), self.stream), "cn_mlp_fwd")
         return sigma, rgb
 
     def new_act(self, M):
         return torch.empty(self.act_bytes(M), dtype=torch.uint8, device=self.device)
 
-    def mlp_bwd(self, blob, M, dsigma, drgb, act):
-        check(self.L.cn_mlp_bwd(self._plan, ptr(self.pack_bwd), ptr(blob), M, ptr(dsigma), ptr(drgb), ptr(act),
-                                self.stream), "cn_mlp_bwd")
+    def mlp_bwd(self, blob, M, dsigma, drgb, act, codes=False):
+        fn = self.L.cn_mlp_bwd_codes if codes else self.L.cn_mlp_bwd
+        check(fn(self._plan, ptr(self.pack_bwd), ptr(blob), M, ptr(dsigma), ptr(drgb), ptr(act), self.stream),
+              "cn_mlp_bwd")
 
     def mlp_dw(self, act, M, zvec, grads, dbuf, ws=None):
         if ws is None:

@@ -65,12 +65,12 @@ class ImageStep:
         tm = self.timers
         ev = tm.mark("fwd") if tm else None
         sigma, rgb = eng.mlp_fwd(blob, M, rays_o=rays_o, rays_d=viewdirs, z=z, z_stride=z_stride,
-                                 n_samples=N, act=buf["act"])
+                                 n_samples=N, act=buf["act"], codes=not weight_grads)
         if tm:
             tm.done("fwd", ev)
         out_rgb, chunk_loss, dsig, drgb = _eng.render_loss(sigma, rgb, z, R, N, gt, self.chunk, self.white_bg)
         ev = tm.mark("bwd") if tm else None
-        eng.mlp_bwd(blob, M, dsig, drgb, buf["act"])
+        eng.mlp_bwd(blob, M, dsig, drgb, buf["act"], codes=not weight_grads)
         if tm:
             tm.done("bwd", ev)
             ev = tm.mark("dw")

@@ -86,6 +86,20 @@ int cn_mlp_fwd(const cn_plan *plan, const void *d_pack_fwd, const float *d_blob,
 int cn_mlp_bwd(const cn_plan *plan, const void *d_pack_bwd, const float *d_blob, int M,
                const float *d_dsigma, const float *d_drgb, void *d_act, void *stream);
 
+/* ---- codes-only optimisation (src/optimizer.py:75-98: the model is fixed,
+ * only the latent codes are updated).  Same arguments as cn_mlp_fwd /
+ * cn_mlp_bwd (d_act required); the forward stores only what the backward
+ * needs (ReLU masks, sigma pre-activations), the backward only the gradient
+ * planes of the layers fed by a code -- what cn_mlp_dbias reads -- and none of
+ * the weight-gradient operands. */
+int cn_mlp_fwd_codes(const cn_plan *plan, const void *d_pack_fwd, const float *d_blob, int M,
+                     const float *d_xyz, const float *d_viewdir, const float *d_rays_o,
+                     const float *d_rays_d, const float *d_z, int z_stride, int n_samples,
+                     float *d_sigma, float *d_rgb, void *d_act, int act_M, int act_row0,
+                     void *stream);
+int cn_mlp_bwd_codes(const cn_plan *plan, const void *d_pack_bwd, const float *d_blob, int M,
+                     const float *d_dsigma, const float *d_drgb, void *d_act, void *stream);
+
 /* ---- weight / bias gradients, accumulated into d_grads; d_dbuf
  * (num_inject x 256) receives this call's bias gradient of every layer fed by
  * a latent code (input of cn_latent_bwd). */
