@@ -3,9 +3,12 @@
 Workload (BASELINE.json configs[1]): srncar.json network (3 shape blocks,
 1 texture block, W = 256), one 128x128 image per object per step, 64 coarse
 + 64 fine samples per ray (128 MLP evaluations per ray), bf16 MFMA with fp32
-accumulation, synthetic SRN-cars-like data (random target image, camera on a
+accumulation, synthetic SRN-cars-like data (targets ray-cast from an
+ellipsoid object by the SRN-format generator's renderer, cameras on a
 radius-1.3 sphere, focal 131.25, near/far 0.8/1.8; no dataset is available
-offline).  One step = rays -> samples -> CodeNeRF forward -> compositing +
+offline; --config c3 uses the srnchair.json geometry: near/far 1.25/2.75,
+radius 2.0).  ``train_psnr`` is the last timed step's -10 log10(mean chunk
+MSE) (src/trainer.py:99), averaged over ranks.  One step = rays -> samples -> CodeNeRF forward -> compositing +
 chunk-mean MSE (+ code regulariser) -> full backward (dX chain, dW, latent
 layers, code rows) -> [RCCL all-reduce of the gradients when N > 1] -> AdamW
 over the model and both code tables.  ``value`` = ray-samples of all ranks /
@@ -47,7 +50,7 @@ def parse():
     #   c4: optimize.py test-time code optimisation, 50 views x 128^2 x 64
     #       samples per step, fwd + dX only (no weight gradients), bf16
     #   c5: 256^2, 128 + 128 samples, fp32, the image in 8 ray parts
-    ap.add_argument("--config", default="c2", choices=["c2", "c4", "c5"])
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     # rehearsal of the N > 1 path on a one-GPU box: gloo, every rank on cuda:0
@@ -137,16 +140,26 @@ def main():
     focal = 131.25 * H / 128
     R = H * W
     timers = Timers()
-    core = TrainCore(model, shape_codes, texture_codes, near=0.8, far=1.8, n_coarse=args.n_coarse,
+    # C3 = srnchair.json geometry (near/far 1.25/2.75, cameras at radius 2.0)
+    near, far, radius = (1.25, 2.75, 2.0) if args.config == "c3" else (0.8, 1.8, 1.3)
+    core = TrainCore(model, shape_codes, texture_codes, near=near, far=far, n_coarse=args.n_coarse,
                      n_fine=args.n_fine, chunk=2048, reg_coef=1e-4, lr=(1e-4, 1e-3), timers=timers,
                      dist=dist)
-    # synthetic views: random targets, poses on the radius-1.3 sphere
+    # synthetic views: a ray-cast ellipsoid object per rank (the SRN-format
+    # generator's renderer, data.make_synthetic_srn) from poses on the sphere
+    import numpy as np
+    from codenerf_amd.data import _object_spec, _render_object
     g = torch.Generator(device="cpu").manual_seed(99 + rank)
+    spec = _object_spec(np.random.Generator(np.random.PCG64(99 + rank)))
     n_views = 8
-    gts = [torch.rand(R, 3, generator=g).to(dev) for _ in range(n_views)]
-    poses = [make_pose(1.3, float(torch.rand(1, generator=g)) * 360 - 180,
-                       float(torch.rand(1, generator=g)) * 50 - 10).to(dev) for _ in range(n_views)]
 
+    def view():
+        c2w = make_pose(radius, float(torch.rand(1, generator=g)) * 360 - 180,
+                        float(torch.rand(1, generator=g)) * 50 - 10)
+        img = _render_object(spec, c2w.double().numpy(), H, W, focal)
+        return c2w.to(dev), torch.tensor(img.reshape(R, 3), dtype=torch.float32, device=dev)
+
+    poses, gts = map(list, zip(*[view() for _ in range(n_views)]))
     ray_parts = 8 if args.config == "c5" else 1
     views_per_step = 50 if args.config == "c4" else 1
     if args.config == "c4":
@@ -159,9 +172,11 @@ def main():
         sc1 = torch.nn.Parameter(shape_codes.detach()[:1].clone())
         tc1 = torch.nn.Parameter(texture_codes.detach()[:1].clone())
         copt = FusedAdamW([{"params": [sc1], "lr": 1e-2}, {"params": [tc1], "lr": 1e-2}])
-        poses += [make_pose(1.3, float(torch.rand(1, generator=g)) * 360 - 180,
-                            float(torch.rand(1, generator=g)) * 50 - 10).to(dev) for _ in range(50 - n_views)]
-        gts += [gts[k % n_views] for k in range(50 - n_views)]
+        extra = [view() for _ in range(50 - n_views)]
+        poses += [e[0] for e in extra]
+        gts += [e[1] for e in extra]
+
+    last = {}
 
     def step(i):
         if args.config == "c4":
@@ -169,12 +184,15 @@ def main():
             tc1.grad = torch.zeros_like(tc1)
             for v in range(views_per_step):
                 ro, vd = _eng.get_rays_dev(H, W, focal, True, poses[v])
-                img.forward_backward(ro, vd, core.stratified_z(dev), gts[v], sc1, tc1, 0, weight_grads=False)
+                loss, _, _ = img.forward_backward(ro, vd, core.stratified_z(dev), gts[v], sc1, tc1, 0,
+                                                  weight_grads=False)
+                last.setdefault("views", []).append(loss)
             copt.step()
+            last["losses"] = torch.cat(last.pop("views"))
             return
         v = i % n_views
         obj = object_for(i, rank, world, n_obj)
-        core.train_step(H, W, focal, poses[v], gts[v], obj, ray_parts=ray_parts)
+        last["losses"] = core.train_step(H, W, focal, poses[v], gts[v], obj, ray_parts=ray_parts)[0]
 
     for i in range(args.warmup):
         step(i)
@@ -198,6 +216,16 @@ def main():
     samples_per_step = R * (args.n_coarse + args.n_fine) * views_per_step
     value = samples_per_step * world * args.steps / dt
     ms = dt / args.steps * 1e3
+
+    # train PSNR of the last timed step (src/trainer.py:99: -10 log10 of the
+    # mean of the chunk MSEs; the fine pass's losses when n_fine > 0)
+    ls = last["losses"]
+    ls = ls[1] if isinstance(ls, tuple) else ls
+    train_psnr = float(-10 * torch.log10(ls.float().mean()))
+    if dist is not None:
+        t = torch.tensor([train_psnr], device=dev, dtype=torch.float64)
+        dist.all_reduce(t)
+        train_psnr = float(t.item()) / world
 
     summ = timers.summary()
     kern = {k: v[0] for k, v in summ.items()}                     # ms per launch
@@ -235,14 +263,17 @@ def main():
     if rank == 0:
         metric = {"c2": "ray-samples/sec (train step), SRN-cars 128x128, 64 coarse + 64 fine samples",
                   "c4": "ray-samples/sec (optimize.py code optimisation step), 50 views x 128x128 x 64 samples",
+                  "c3": "ray-samples/sec (train step), SRN-chairs geometry 128x128, 64 coarse + 64 fine samples",
                   "c5": "ray-samples/sec (train step), SRN-cars 256x256, 128 coarse + 128 fine samples, fp32"}
         out = {
             "metric": metric[args.config],
             "value": round(value, 1), "unit": "ray-samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
-            "data": f"synthetic (random {H}x{W} targets, poses on a radius-1.3 sphere, random-init weights)",
-            "config": {"workload": f"srncar.json net, {H}x{W} image/object/step, {args.n_coarse}+{args.n_fine} "
+            "data": f"synthetic ({H}x{W} ray-cast ellipsoid object per rank, poses on a radius-{radius} sphere, "
+                    f"random-init weights)",
+            "train_psnr": round(train_psnr, 3),
+            "config": {"workload": f"{'srnchair' if args.config == 'c3' else 'srncar'}.json net, {H}x{W} image/object/step, {args.n_coarse}+{args.n_fine} "
                                    f"samples/ray, " + ("50 views, codes-only fwd+dX+AdamW" if args.config == "c4"
                                                        else "train step incl. AdamW"),
                        "name": args.config, "objects_per_step": world,

@@ -44,6 +44,10 @@ CN_DEV void glds16(const void* gsrc, lds_void* ldst) {
 CN_DEV void glds16_opaque(const void* gsrc, uint32_t lds_byte) {
   asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "{m0}"(lds_byte) : "memory");
 }
+// The same with the non-temporal policy, for once-read streams.
+CN_DEV void glds16_opaque_nt(const void* gsrc, uint32_t lds_byte) {
+  asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(gsrc), "{m0}"(lds_byte) : "memory");
+}
 CN_DEV uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)(lds_void*)p; }
 
 template <int N>

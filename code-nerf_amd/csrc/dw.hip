@@ -22,6 +22,10 @@
 #include "chain_args.h"
 #include "dw_args.h"
 
+#ifndef CN_DW_NT
+#define CN_DW_NT 1      // non-temporal policy on the once-read operand stream (A/B: 3.24 -> 3.13 ms per C2 dW)
+#endif
+
 namespace cn {
 
 typedef __attribute__((ext_vector_type(4))) short s16x4;
@@ -132,7 +136,11 @@ struct DwBody {
           src = pa + t * (kA * TB);              // padding piece: re-read, never consumed
           dst = lds_addr(smem + kDwDummy + (piece - kPieces) * 1024);
         }
+#if CN_DW_NT
+        glds16_opaque_nt(src + lane * 16, dst);
+#else
         glds16_opaque(src + lane * 16, dst);
+#endif
       }
     };
     static_for<0, kDwDepth>([&](auto i) {

@@ -98,6 +98,30 @@ def test_train_psnr_matches_cpu_replay(tmp_path):
     assert "weight" in ck["shape_code_params"]
 
 
+def test_bf16_train_psnr_within_005db_of_fp32_replay(tmp_path):
+    """north_star: "PSNR within 0.05 dB of reference" for the bf16 (C2) path:
+    the bf16-MFMA trainer against the fp32 CPU replay of the reference loop
+    on the same data, initial weights and RNG draws."""
+    from codenerf_amd.data import make_synthetic_srn
+    from codenerf_amd.trainer import Trainer
+    root = str(tmp_path / "data")
+    make_synthetic_srn(root, "srn_cars", "cars_train", n_obj=2, n_views=4, H=32, W=32, focal=32.8, seed=5)
+    hp = _hpams(root, N=64, prec="bf16")
+    tr = Trainer("t", 0, hpams=hp, batch_size=256, check_iter=0, exp_root=str(tmp_path / "exps"))
+    init = {"model": {k: v.detach().cpu().clone() for k, v in tr.model.state_dict().items()},
+            "shape": tr.shape_codes.weight.detach().cpu().clone(),
+            "texture": tr.texture_codes.weight.detach().cpu().clone()}
+    iters = 8
+    torch.manual_seed(7)
+    np.random.seed(7)
+    tr.training(0, iters, 1)
+    torch.manual_seed(7)
+    np.random.seed(7)
+    ref_psnr, _, _, _ = _oracle_training(hp, init, iters, 256)
+    assert len(tr.psnr_log) == len(ref_psnr) == iters
+    np.testing.assert_allclose(np.array(tr.psnr_log), np.array(ref_psnr), atol=0.05)
+
+
 def test_codes_only_backward_matches_full():
     from codenerf_amd.model import CodeNeRF
     from codenerf_amd.render import ImageStep
