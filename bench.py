@@ -242,7 +242,7 @@ def main():
         roof = {"bound": "mfma", "kernel": {"fwd": "chain_kernel<fwd,train>", "bwd": "chain_kernel<bwd>",
                                             "dw": "dw_kernel"}[dom],
                 "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4), "traffic": load_traffic(dom),
+                "frac": round(achieved / peak, 4), "traffic": load_traffic(args.config, dom),
                 "ms_per_launch": {k: round(v, 4) for k, v in kern.items()},
                 "ms_per_step_by_phase": {k: round(v, 4) for k, v in per_step.items()}}
         if dom == "dw" and args.precision == "bf16":
@@ -286,13 +286,13 @@ def main():
         dist.destroy_process_group()
 
 
-def load_traffic(kernel):
+def load_traffic(config, kernel):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3
-    PMC summary (profiles/*pmc*.json), or None."""
+    PMC summary of the same config (profiles/pmc_traffic.json), or None."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            return json.load(f).get(kernel)
+            return json.load(f).get(config, {}).get(kernel)
     except OSError:
         return None
 

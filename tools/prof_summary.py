@@ -58,7 +58,8 @@ def main():
             traffic[s] = {"hbm_bytes": int(hbm), "fetch_kib": f, "write_kib": w, "avg_ns": avg_ns,
                           "source": f"profiles/{tag}_kernels.md"}
     open(os.path.join(prof, f"{tag}_kernels.md"), "w").write("\n".join(lines) + "\n")
-    json.dump(traffic, open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1)
+    # keyed by bench config (the profiled command is bench.py's default, C2)
+    json.dump({"c2": traffic}, open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1)
     print("\n".join(lines[:16]))
 
 
