@@ -186,7 +186,8 @@ int cn_mlp_fwd_codes(const cn_plan* p, const void* d_pack, const float* d_blob, 
 }
 
 static int mlp_bwd_impl(int codes, const cn_plan* p, const void* d_pack, const float* d_blob, int M,
-                        const float* d_dsigma, const float* d_drgb, void* d_act, void* stream) {
+                        const float* d_dsigma, const float* d_drgb, void* d_act, int act_M, int act_row0,
+                        void* stream) {
   if (!p || !d_pack || !d_blob || !d_dsigma || !d_drgb || !d_act) return fail("cn_mlp_bwd: NULL argument");
   if (M <= 0) return fail("cn_mlp_bwd: M must be positive");
   ChainArgs a{};
@@ -196,14 +197,24 @@ static int mlp_bwd_impl(int codes, const cn_plan* p, const void* d_pack, const f
   a.dsigma = d_dsigma;
   a.drgb = d_drgb;
   const int Mp = cn_pad_samples(p, M);
-  const ActLayout L = p->cs.layout(Mp);
+  // rows [act_row0, act_row0 + Mp) of a workspace laid out for act_M samples
+  if (act_M <= 0) act_M = M;
+  if (act_row0 < 0 || act_row0 % p->cs.tile) return fail("cn_mlp_bwd: act_row0 must be a multiple of the tile");
+  const int Ma = cn_pad_samples(p, act_M);
+  if (act_row0 + Mp > Ma) return fail("cn_mlp_bwd: rows exceed the activation workspace");
+  const ActLayout L = p->cs.layout(Ma);
+  const size_t es = p->cs.prec ? 2 : 4;
+  const size_t r0 = (size_t)act_row0;
   char* b = (char*)d_act;
-  a.pe = b + L.pe;
-  a.dir = b + L.dir;
-  for (int i = 0; i < kMaxPlanes; ++i) { a.Y[i] = b + L.Y[i]; a.dA[i] = b + L.dA[i]; }
-  a.d8 = b + L.d8;
-  a.spre = (float*)(b + L.spre);
-  a.masks = (uint32_t*)(b + L.masks);
+  a.pe = b + L.pe + r0 * 64 * es;
+  a.dir = b + L.dir + r0 * 32 * es;
+  for (int i = 0; i < kMaxPlanes; ++i) {
+    a.Y[i] = b + L.Y[i] + r0 * L.Yw[i] * es;
+    a.dA[i] = b + L.dA[i] + r0 * L.dAw[i] * es;
+  }
+  a.d8 = b + L.d8 + r0 * 32 * es;
+  a.spre = (float*)(b + L.spre) + r0;
+  a.masks = (uint32_t*)(b + L.masks + (r0 / 32) * L.mask_bytes_per_slab);
   hipLaunchKernelGGL(codes ? p->cs.bwd_codes : p->cs.bwd, dim3(Mp / p->cs.tile), dim3(p->cs.waves * 64), 0,
                      S(stream), a);
   return launch_check("chain_kernel(bwd)");
@@ -211,28 +222,47 @@ static int mlp_bwd_impl(int codes, const cn_plan* p, const void* d_pack, const f
 
 int cn_mlp_bwd(const cn_plan* p, const void* d_pack, const float* d_blob, int M, const float* d_dsigma,
                const float* d_drgb, void* d_act, void* stream) {
-  return mlp_bwd_impl(0, p, d_pack, d_blob, M, d_dsigma, d_drgb, d_act, stream);
+  return mlp_bwd_impl(0, p, d_pack, d_blob, M, d_dsigma, d_drgb, d_act, M, 0, stream);
+}
+
+int cn_mlp_bwd_rows(const cn_plan* p, const void* d_pack, const float* d_blob, int M, const float* d_dsigma,
+                    const float* d_drgb, void* d_act, int act_M, int act_row0, void* stream) {
+  return mlp_bwd_impl(0, p, d_pack, d_blob, M, d_dsigma, d_drgb, d_act, act_M, act_row0, stream);
 }
 
 int cn_mlp_bwd_codes(const cn_plan* p, const void* d_pack, const float* d_blob, int M, const float* d_dsigma,
                      const float* d_drgb, void* d_act, void* stream) {
-  return mlp_bwd_impl(1, p, d_pack, d_blob, M, d_dsigma, d_drgb, d_act, stream);
+  return mlp_bwd_impl(1, p, d_pack, d_blob, M, d_dsigma, d_drgb, d_act, M, 0, stream);
 }
 
-int cn_mlp_dw(const cn_plan* p, void* d_act, int M, const float* d_zvec, float* const* d_grads, float* d_dbuf,
-              void* d_ws, void* stream) {
+static int mlp_dw_impl(const cn_plan* p, void* d_act, int act_M, int act_row0, int M, const float* d_zvec,
+                       float* const* d_grads, float* d_dbuf, int db_accum, void* d_ws, void* stream) {
   if (!p || !d_act || !d_zvec || !d_grads || !d_dbuf || !d_ws) return fail("cn_mlp_dw: NULL argument");
   if (M <= 0) return fail("cn_mlp_dw: M must be positive");
+  if (act_M <= 0) act_M = M;
+  if (act_row0 < 0 || act_row0 % 256 || act_row0 + cn_pad_samples(p, M) > cn_pad_samples(p, act_M))
+    return fail("cn_mlp_dw: rows exceed the activation workspace (act_row0 must be a multiple of 256)");
   DwArgs dw;
   DwRedArgs red;
-  const int nwg = p->cs.dw_setup((char*)d_act, M, d_zvec, d_dbuf, (char*)d_ws, &dw, &red);
+  const int nwg = p->cs.dw_setup((char*)d_act, act_M, act_row0, M, d_zvec, d_dbuf, (char*)d_ws, &dw, &red);
   if (nwg <= 0) return fail("cn_mlp_dw: schedule does not fit the partial workspace");
   red.grads = d_grads;
+  red.db_accum = db_accum ? 1 : 0;
   if (p->cs.prec) hipLaunchKernelGGL(dw_kernel<CN_P_BF16>, dim3(nwg), dim3(512), 0, S(stream), dw);
   else hipLaunchKernelGGL(dw_kernel<CN_P_FP32>, dim3(nwg), dim3(512), 0, S(stream), dw);
   if (launch_check("dw_kernel")) return -1;
   hipLaunchKernelGGL(dw_reduce_kernel, dim3(grid_for(red.prefix[red.nprob], 256)), dim3(256), 0, S(stream), red);
   return launch_check("dw_reduce_kernel");
+}
+
+int cn_mlp_dw(const cn_plan* p, void* d_act, int M, const float* d_zvec, float* const* d_grads, float* d_dbuf,
+              void* d_ws, void* stream) {
+  return mlp_dw_impl(p, d_act, M, 0, M, d_zvec, d_grads, d_dbuf, 0, d_ws, stream);
+}
+
+int cn_mlp_dw_rows(const cn_plan* p, void* d_act, int act_M, int act_row0, int M, const float* d_zvec,
+                   float* const* d_grads, float* d_dbuf, int db_accum, void* d_ws, void* stream) {
+  return mlp_dw_impl(p, d_act, act_M, act_row0, M, d_zvec, d_grads, d_dbuf, db_accum, d_ws, stream);
 }
 
 int cn_mlp_dbias(const cn_plan* p, void* d_act, int M, float* d_dbuf, void* d_ws, void* stream) {

@@ -39,7 +39,7 @@ struct ChainSet {
   std::vector<int32_t> (*bwd_table)() = nullptr;
   ActLayout (*layout)(size_t Mp) = nullptr;
   // fills the dW / reduce argument blocks; returns the number of dW workgroups
-  int (*dw_setup)(char* act, int M, const float* zvec, float* dbuf, char* ws, DwArgs* dw,
+  int (*dw_setup)(char* act, int act_M, int row0, int M, const float* zvec, float* dbuf, char* ws, DwArgs* dw,
                   DwRedArgs* red) = nullptr;
   size_t (*dw_ws_bytes)(int M) = nullptr;
   // fills the bias-only argument block (dbuf rows of the injection layers)

@@ -106,13 +106,20 @@ size_t dw_ws_bytes(int) {
   return (size_t)kDwWorkgroups * 2 * ((size_t)kPartRows * kPartCols + kPartRows) * sizeof(float);
 }
 
+// Rows [row0, row0 + pad(M)) of a workspace laid out for act_M samples
+// (row0 a multiple of 256): the coarse and fine row ranges of one step can
+// then be reduced by two launches, each overlapping the other range's dX chain.
 template <int P, int SB, int TB>
-int dw_setup(char* act, int M, const float* zvec, float* dbuf, char* ws, DwArgs* dw, DwRedArgs* red) {
+int dw_setup(char* act, int act_M, int row0, int M, const float* zvec, float* dbuf, char* ws, DwArgs* dw,
+             DwRedArgs* red) {
   using N = Net<SB, TB>;
   constexpr ParamIdx PI{SB, TB};
   constexpr int ES = P == CN_P_BF16 ? 2 : 4;
   const int Mp = ((M + 255) / 256) * 256;
-  const ActLayout A = act_layout<P, SB, TB>(Mp);
+  const int Ma = ((act_M + 255) / 256) * 256;
+  if (row0 < 0 || row0 % 256 || row0 + Mp > Ma) return -1;
+  const ActLayout A = act_layout<P, SB, TB>(Ma);
+  const size_t r0 = (size_t)row0 * ES;      // byte offset per element of plane width
   static_assert(N::kFwdLayers <= kDwMaxProblems, "dw problems");
   *dw = DwArgs{};
   *red = DwRedArgs{};
@@ -124,14 +131,14 @@ int dw_setup(char* act, int M, const float* zvec, float* dbuf, char* ws, DwArgs*
     const bool last = L == N::kFwdLayers - 1;
     const bool vd = L == SB + 2;
     DwProblem& p = dw->p[L];
-    p.A = act + (last ? A.d8 : A.dA[L]);
     p.a_width = last ? 32 : N::dplane_width(L);
+    p.A = act + (last ? A.d8 : A.dA[L]) + r0 * p.a_width;
     p.a_tiles = p.a_width / 32;
     p.out_tiles = last ? 1 : N::fwd(L).T;
-    if (L == 0) { p.X0 = act + A.pe; p.x0_width = 64; }
-    else { p.X0 = act + A.Y[L - 1]; p.x0_width = N::plane_width(L - 1); }
+    if (L == 0) { p.X0 = act + A.pe + r0 * 64; p.x0_width = 64; }
+    else { p.x0_width = N::plane_width(L - 1); p.X0 = act + A.Y[L - 1] + r0 * p.x0_width; }
     p.x0_tiles = p.x0_width / 32;
-    if (vd) { p.X1 = act + A.dir; p.x1_width = 32; p.x1_tiles = 1; }
+    if (vd) { p.X1 = act + A.dir + r0 * 32; p.x1_width = 32; p.x1_tiles = 1; }
     p.sigma_head = vd ? 1 : 0;
     p.kind = L == 0 ? DW_PE : vd ? DW_VIEWDIR : last ? DW_RGB2 : (L == N::kFwdLayers - 2 ? DW_RGB0 : DW_FULL);
     {

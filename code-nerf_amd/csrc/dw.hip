@@ -346,7 +346,7 @@ __global__ __launch_bounds__(256) void dw_reduce_kernel(DwRedArgs a) {
   if (f >= 0 && f < p.in_real) a.grads[p.w][(size_t)n * p.in_real + f] += v;
   if (c == 0) {
     a.grads[p.b][n] += db;
-    if (p.dbout) p.dbout[n] = db;
+    if (p.dbout) p.dbout[n] = a.db_accum ? p.dbout[n] + db : db;
   }
 }
 

@@ -92,6 +92,7 @@ struct DwRedArgs {
   // workgroups holding slabs of problem p: gfirst[p] .. glast[p]; the first
   // one may hold it as its second segment (gseg[p]), the others as their first
   int gfirst[kDwMaxProblems], glast[kDwMaxProblems], gseg[kDwMaxProblems];
+  int db_accum;                 // dbout += (a later row range of the same step) instead of =
 };
 
 // Bias gradients of the layers that follow a code injection only (codes-only

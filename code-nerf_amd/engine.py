@@ -122,6 +122,18 @@ class Engine:
         check(fn(self._plan, ptr(self.pack_bwd), ptr(blob), M, ptr(dsigma), ptr(drgb), ptr(act), self.stream),
               "cn_mlp_bwd")
 
+    def mlp_bwd_rows(self, blob, M, dsigma, drgb, act, act_M, row0):
+        """dX chain over rows [row0, row0 + pad(M)) of an act_M-sample
+        workspace; dsigma / drgb hold the range's rows."""
+        check(self.L.cn_mlp_bwd_rows(self._plan, ptr(self.pack_bwd), ptr(blob), M, ptr(dsigma), ptr(drgb), ptr(act),
+                                     act_M, row0, self.stream), "cn_mlp_bwd_rows")
+
+    def mlp_dw_rows(self, act, act_M, row0, M, zvec, grads, dbuf, ws, db_accum=False):
+        """Weight gradients over rows [row0, row0 + pad(M)) (grads and, with
+        db_accum, dbuf accumulate)."""
+        check(self.L.cn_mlp_dw_rows(self._plan, ptr(act), act_M, row0, M, ptr(zvec), ptr(self.table(grads)),
+                                    ptr(dbuf), int(bool(db_accum)), ptr(ws), self.stream), "cn_mlp_dw_rows")
+
     def mlp_dw(self, act, M, zvec, grads, dbuf, ws=None):
         if ws is None:
             ws = torch.empty(self.dw_ws_bytes(M), dtype=torch.uint8, device=self.device)

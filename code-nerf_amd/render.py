@@ -16,8 +16,12 @@ from . import engine as _eng
 
 
 class ImageStep:
-    def __init__(self, model, chunk=2048, reg_coef=1e-4, white_bg=True, timers=None):
+    def __init__(self, model, chunk=2048, reg_coef=1e-4, white_bg=True, timers=None, overlap_dw=True):
         self.model = model
+        # coarse + fine step: weight gradients of the fine rows on a second
+        # stream while the dX chain runs over the coarse rows
+        self.overlap_dw = bool(overlap_dw)
+        self._side = None
         self.timers = timers
         self.chunk = int(chunk)
         self.reg_coef = float(reg_coef)
@@ -138,19 +142,58 @@ class ImageStep:
         out_f, loss_f = _eng.render_loss_fine(sig_c, rgb_c, z_c, Nc, sig_f, rgb_f, z_f, Nf, R, gt, self.chunk,
                                               dsig[:Mc], drgb[:Mc], dsig[Mc_p:Mc_p + Mf],
                                               drgb[Mc_p:Mc_p + Mf], self.white_bg)
-        ev = tm.mark("bwd") if tm else None
-        eng.mlp_bwd(blob, M, dsig, drgb, buf["act"])
-        if tm:
-            tm.done("bwd", ev)
-            ev = tm.mark("dw")
-        eng.mlp_dw(buf["act"], M, zvec, grads, buf["dbuf"], buf["dw"])
-        if tm:
-            tm.done("dw", ev)
+        if self.overlap_dw:
+            self._bwd_dw_overlapped(eng, blob, buf, dsig, drgb, zvec, grads, Mc, Mc_p, Mf, M)
+        else:
+            ev = tm.mark("bwd") if tm else None
+            eng.mlp_bwd(blob, M, dsig, drgb, buf["act"])
+            if tm:
+                tm.done("bwd", ev)
+                ev = tm.mark("dw")
+            eng.mlp_dw(buf["act"], M, zvec, grads, buf["dbuf"], buf["dw"])
+            if tm:
+                tm.done("dw", ev)
         reg_out = torch.zeros(1, dtype=torch.float32, device=eng.device)
         eng.latent_bwd(params, grads, s, t, zvec, buf["dbuf"], shape_table.grad[obj_idx],
                        texture_table.grad[obj_idx], self.reg_coef if reg else 0.0, reg_out)
         self.last_z_f = z_f
         return loss_c, loss_f, out_f, reg_out
+
+    def _bwd_dw_overlapped(self, eng, blob, buf, dsig, drgb, zvec, grads, Mc, Mc_p, Mf, M):
+        """dX chain over the fine rows, then (current stream) the dX chain over
+        the coarse rows while (side stream) dW reduces the fine rows, then dW
+        of the coarse rows.  Same rows and sums as one mlp_bwd + mlp_dw over
+        [0, M); the fp32 partial order differs.  dW is HBM-bound (operand
+        stream), the dX chain MFMA-bound, so the two share the chip."""
+        tm = self.timers
+        act = buf["act"]
+        main = torch.cuda.current_stream(eng.device)
+        if self._side is None:
+            self._side = torch.cuda.Stream(eng.device)
+        side = self._side
+        ev = tm.mark("bwd") if tm else None
+        eng.mlp_bwd_rows(blob, Mf, dsig[Mc_p:], drgb[Mc_p:], act, M, Mc_p)
+        fine_done = torch.cuda.Event()
+        fine_done.record(main)
+        side.wait_event(fine_done)
+        eng.mlp_bwd_rows(blob, Mc, dsig, drgb, act, M, 0)
+        if tm:
+            tm.done("bwd", ev)
+        coarse_done = torch.cuda.Event()
+        coarse_done.record(main)
+        with torch.cuda.stream(side):
+            # timers: one span per dW launch, each from the moment its rows are
+            # ready (and the side stream free) to its end
+            ev = tm.mark("dw") if tm else None
+            eng.mlp_dw_rows(act, M, Mc_p, Mf, zvec, grads, buf["dbuf"], buf["dw"], db_accum=False)
+            if tm:
+                tm.done("dw", ev)
+            side.wait_event(coarse_done)
+            ev = tm.mark("dw") if tm else None
+            eng.mlp_dw_rows(act, M, 0, Mc, zvec, grads, buf["dbuf"], buf["dw"], db_accum=True)
+            if tm:
+                tm.done("dw", ev)
+        main.wait_stream(side)
 
     @torch.no_grad()
     def render(self, rays_o, viewdirs, z_vals, shape_code, texture_code):

@@ -86,6 +86,16 @@ int cn_mlp_fwd(const cn_plan *plan, const void *d_pack_fwd, const float *d_blob,
 int cn_mlp_bwd(const cn_plan *plan, const void *d_pack_bwd, const float *d_blob, int M,
                const float *d_dsigma, const float *d_drgb, void *d_act, void *stream);
 
+/* ---- the same over rows [act_row0, act_row0 + pad(M)) of a workspace laid
+ * out for act_M samples (act_row0 a multiple of 256); d_dsigma / d_drgb point
+ * at the range's first row.  The coarse and fine rows of one training step
+ * (src/trainer.py:82 over both passes) are back-propagated by two launches so
+ * the weight gradients of the first range (cn_mlp_dw_rows, on a second
+ * stream) overlap the dX chain of the second. */
+int cn_mlp_bwd_rows(const cn_plan *plan, const void *d_pack_bwd, const float *d_blob, int M,
+                    const float *d_dsigma, const float *d_drgb, void *d_act, int act_M, int act_row0,
+                    void *stream);
+
 /* ---- codes-only optimisation (src/optimizer.py:75-98: the model is fixed,
  * only the latent codes are updated).  Same arguments as cn_mlp_fwd /
  * cn_mlp_bwd (d_act required); the forward stores only what the backward
@@ -105,6 +115,14 @@ int cn_mlp_bwd_codes(const cn_plan *plan, const void *d_pack_bwd, const float *d
  * a latent code (input of cn_latent_bwd). */
 int cn_mlp_dw(const cn_plan *plan, void *d_act, int M, const float *d_zvec,
               float *const *d_grads, float *d_dbuf, void *d_ws, void *stream);
+
+/* ---- cn_mlp_dw over rows [act_row0, act_row0 + pad(M)) of a workspace laid
+ * out for act_M samples (act_row0 a multiple of 256).  db_accum != 0 adds
+ * this range's bias gradients into d_dbuf instead of overwriting it (the
+ * second range of a step).  Grads accumulate as in cn_mlp_dw. */
+int cn_mlp_dw_rows(const cn_plan *plan, void *d_act, int act_M, int act_row0, int M,
+                   const float *d_zvec, float *const *d_grads, float *d_dbuf, int db_accum,
+                   void *d_ws, void *stream);
 
 /* ---- bias gradients of the layers after each code injection only (d_dbuf
  * [n_inject][256], as cn_mlp_dw writes them), for codes-only optimisation

@@ -92,7 +92,7 @@ def test_render_loss_fine_matches_oracle(Nc, Nf, chunk):
     np.testing.assert_allclose(drf.cpu().reshape(R, Nf, 3).numpy(), rf.grad.numpy(), rtol=1e-4, atol=1e-8)
 
 
-def _fine_step(g, precision, Nf, rnd):
+def _fine_step(g, precision, Nf, rnd, overlap_dw=True):
     from codenerf_amd.model import CodeNeRF
     from codenerf_amd.render import ImageStep
     m = CodeNeRF(3, 1, precision=precision)
@@ -100,7 +100,7 @@ def _fine_step(g, precision, Nf, rnd):
     m = m.to(_dev())
     st = torch.nn.Parameter(torch.tensor(g["shape_table"], device=_dev()))
     tt = torch.nn.Parameter(torch.tensor(g["texture_table"], device=_dev()))
-    step = ImageStep(m, chunk=int(g["chunk"]), reg_coef=1e-4)
+    step = ImageStep(m, chunk=int(g["chunk"]), reg_coef=1e-4, overlap_dw=overlap_dw)
     ro = torch.tensor(g["rays_o"], device=_dev())
     vd = torch.tensor(g["viewdir"], device=_dev())
     z = torch.tensor(g["z_vals"], device=_dev())
@@ -157,3 +157,23 @@ def test_fine_train_step_bf16_close_to_fp32():
         if b.grad.abs().max() > 0:
             a_, b_ = a.grad.reshape(-1).double(), b.grad.reshape(-1).double()
             assert float(a_ @ b_ / (a_.norm() * b_.norm())) > 0.98, k
+
+
+@pytest.mark.parametrize("precision,case,Nf", [("fp32", "ragged_48x48_n16", 40), ("bf16", "n64_16x16", 64),
+                                               ("bf16", "chunks_64x64_n16", 16)])
+def test_overlapped_bwd_dw_matches_single_pass(precision, case, Nf):
+    """ImageStep(overlap_dw=True): dX chain + dW split at the coarse / fine
+    row boundary on two streams (cn_mlp_bwd_rows / cn_mlp_dw_rows) gives the
+    gradients of the one-launch path (same sums, fp32 partial order aside)."""
+    g = load(case)
+    R = g["rays_o"].shape[0]
+    rnd = torch.rand(R, Nf, generator=torch.Generator().manual_seed(8))
+    a = _fine_step(g, precision, Nf, rnd, overlap_dw=True)
+    b = _fine_step(g, precision, Nf, rnd, overlap_dw=False)
+    np.testing.assert_array_equal(a[4].cpu().numpy(), b[4].cpu().numpy())      # fine losses
+    for (k, pa), (_, pb) in zip(a[0].named_parameters(), b[0].named_parameters()):
+        x, y = pa.grad.cpu().numpy(), pb.grad.cpu().numpy()
+        np.testing.assert_allclose(x, y, rtol=1e-4, atol=1e-5 * max(1e-30, np.abs(y).max()), err_msg=k)
+    for i in (1, 2):
+        x, y = a[i].grad.cpu().numpy(), b[i].grad.cpu().numpy()
+        np.testing.assert_allclose(x, y, rtol=1e-4, atol=1e-5 * max(1e-30, np.abs(y).max()))
