@@ -39,8 +39,8 @@ DW_BYTES_PER_SAMPLE = 8_000     # bf16 dA + X operand planes read by dw_kernel (
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--H", type=int, default=128)
     ap.add_argument("--n-coarse", type=int, default=64)
     ap.add_argument("--n-fine", type=int, default=64)
@@ -53,8 +53,13 @@ def parse():
     ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-overlap", action="store_true",
-                    help="one dX launch then one dW launch (no coarse/fine two-stream overlap)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+                    help="one dX launch then one dW launch (no two-stream dX / dW pipelining)")
+    ap.add_argument("--bwd-ranges", type=int, default=None, help="row ranges of the dX / dW pipeline")
+    ap.add_argument("--dw-side-wgs", type=int, default=None,
+                    help="persistent workgroups of the dW launches that run beside a dX chain (0: 256)")
+    ap.add_argument("--no-fp32", action="store_true", help="skip the secondary fp32 figure of the C2 step")
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="CPU baseline threads (default: OMP_NUM_THREADS, else all host CPUs)")
     # rehearsal of the N > 1 path on a one-GPU box: gloo, every rank on cuda:0
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--one-device", action="store_true")
@@ -105,6 +110,112 @@ class Timers:
         return out
 
 
+def build_workload(args, dev, rank, world, precision, timers, dist):
+    """Model, codes, synthetic views and the step closure of one bench config."""
+    from codenerf_amd.model import CodeNeRF
+    from codenerf_amd.trainer_core import TrainCore
+    from codenerf_amd.dp import broadcast_from, object_for
+
+    torch.manual_seed(1234 + rank)
+    model = CodeNeRF(3, 1, precision=precision).to(dev)
+    n_obj = args.objects
+    shape_codes = torch.nn.Parameter(torch.randn(n_obj, 256, device=dev) / math.sqrt(128))
+    texture_codes = torch.nn.Parameter(torch.randn(n_obj, 256, device=dev) / math.sqrt(128))
+    # identical initial weights and codes on every rank
+    broadcast_from(list(model.parameters()) + [shape_codes, texture_codes], dist)
+
+    H = W = args.H
+    focal = 131.25 * H / 128
+    R = H * W
+    # C3 = srnchair.json geometry (near/far 1.25/2.75, cameras at radius 2.0)
+    near, far, radius = (1.25, 2.75, 2.0) if args.config == "c3" else (0.8, 1.8, 1.3)
+    opts = dict(overlap_dw=not args.no_overlap)
+    if args.bwd_ranges is not None:
+        opts["bwd_ranges"] = args.bwd_ranges
+    if args.dw_side_wgs is not None:
+        opts["dw_side_wgs"] = args.dw_side_wgs
+    core = TrainCore(model, shape_codes, texture_codes, near=near, far=far, n_coarse=args.n_coarse,
+                     n_fine=args.n_fine, chunk=2048, reg_coef=1e-4, lr=(1e-4, 1e-3), timers=timers,
+                     dist=dist, step_opts=opts)
+    # synthetic views: a ray-cast ellipsoid object per rank (the SRN-format
+    # generator's renderer, data.make_synthetic_srn) from poses on the sphere
+    import numpy as np
+    from codenerf_amd.data import _object_spec, _render_object
+    g = torch.Generator(device="cpu").manual_seed(99 + rank)
+    spec = _object_spec(np.random.Generator(np.random.PCG64(99 + rank)))
+    n_views = 50 if args.config == "c4" else 8
+
+    def view():
+        c2w = make_pose(radius, float(torch.rand(1, generator=g)) * 360 - 180,
+                        float(torch.rand(1, generator=g)) * 50 - 10)
+        img = _render_object(spec, c2w.double().numpy(), H, W, focal)
+        return c2w.to(dev), torch.tensor(img.reshape(R, 3), dtype=torch.float32, device=dev)
+
+    poses, gts = map(list, zip(*[view() for _ in range(n_views)]))
+    last = {}
+    if args.config == "c4":
+        # src/optimizer.py:66-98: codes only (weights fixed), every target view
+        # accumulates into the code gradients, then one AdamW step on the codes
+        from codenerf_amd.optim import FusedAdamW
+        from codenerf_amd.render import ImageStep
+        from codenerf_amd import engine as _eng
+        img = ImageStep(model, chunk=2048, reg_coef=1e-4, timers=timers)
+        sc1 = torch.nn.Parameter(shape_codes.detach()[:1].clone())
+        tc1 = torch.nn.Parameter(texture_codes.detach()[:1].clone())
+        copt = FusedAdamW([{"params": [sc1], "lr": 1e-2}, {"params": [tc1], "lr": 1e-2}])
+
+        def step(i):
+            sc1.grad = torch.zeros_like(sc1)
+            tc1.grad = torch.zeros_like(tc1)
+            views = []
+            for v in range(n_views):
+                ro, vd = _eng.get_rays_dev(H, W, focal, True, poses[v])
+                loss, _, _ = img.forward_backward(ro, vd, core.stratified_z(dev), gts[v], sc1, tc1, 0,
+                                                  weight_grads=False)
+                views.append(loss)
+            copt.step()
+            last["losses"] = torch.cat(views)
+    else:
+        def step(i):
+            v = i % n_views
+            obj = object_for(i, rank, world, n_obj)
+            last["losses"] = core.train_step(H, W, focal, poses[v], gts[v], obj)[0]
+    views_per_step = n_views if args.config == "c4" else 1
+    samples_per_step = R * (args.n_coarse + args.n_fine) * views_per_step
+    return dict(step=step, last=last, core=core, R=R, H=H, radius=radius, samples_per_step=samples_per_step)
+
+
+def timed_run(wl, steps, warmup, timers, dist, dev):
+    """warmup untimed steps, then exactly `steps` steps between barriers +
+    synchronize; per-step HIP events (current stream) give the median."""
+    for i in range(warmup):
+        wl["step"](i)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timers.on = True
+    marks = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    t0 = time.perf_counter()
+    marks[0].record()
+    for i in range(steps):
+        wl["step"](warmup + i)
+        marks[i + 1].record()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    timers.on = False
+    per = sorted(marks[i].elapsed_time(marks[i + 1]) for i in range(steps))
+    median = per[len(per) // 2] if steps % 2 else 0.5 * (per[steps // 2 - 1] + per[steps // 2])
+    if dist is not None:
+        t = torch.tensor([dt, median], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt, median = float(t[0]), float(t[1])
+    return dt, median
+
+
 def main():
     args = parse()
     if args.config == "c4":
@@ -126,103 +237,16 @@ def main():
         else:
             dist.init_process_group("gloo")
 
-    from codenerf_amd.model import CodeNeRF
-    from codenerf_amd.trainer_core import TrainCore
-    from codenerf_amd.dp import broadcast_from, object_for
-
-    torch.manual_seed(1234 + rank)
-    model = CodeNeRF(3, 1, precision=args.precision).to(dev)
-    n_obj = args.objects
-    shape_codes = torch.nn.Parameter(torch.randn(n_obj, 256, device=dev) / math.sqrt(128))
-    texture_codes = torch.nn.Parameter(torch.randn(n_obj, 256, device=dev) / math.sqrt(128))
-    # identical initial weights and codes on every rank
-    broadcast_from(list(model.parameters()) + [shape_codes, texture_codes], dist)
-
-    H = W = args.H
-    focal = 131.25 * H / 128
-    R = H * W
     timers = Timers()
-    # C3 = srnchair.json geometry (near/far 1.25/2.75, cameras at radius 2.0)
-    near, far, radius = (1.25, 2.75, 2.0) if args.config == "c3" else (0.8, 1.8, 1.3)
-    core = TrainCore(model, shape_codes, texture_codes, near=near, far=far, n_coarse=args.n_coarse,
-                     n_fine=args.n_fine, chunk=2048, reg_coef=1e-4, lr=(1e-4, 1e-3), timers=timers,
-                     dist=dist)
-    core.step_impl.overlap_dw = not args.no_overlap
-    # synthetic views: a ray-cast ellipsoid object per rank (the SRN-format
-    # generator's renderer, data.make_synthetic_srn) from poses on the sphere
-    import numpy as np
-    from codenerf_amd.data import _object_spec, _render_object
-    g = torch.Generator(device="cpu").manual_seed(99 + rank)
-    spec = _object_spec(np.random.Generator(np.random.PCG64(99 + rank)))
-    n_views = 8
-
-    def view():
-        c2w = make_pose(radius, float(torch.rand(1, generator=g)) * 360 - 180,
-                        float(torch.rand(1, generator=g)) * 50 - 10)
-        img = _render_object(spec, c2w.double().numpy(), H, W, focal)
-        return c2w.to(dev), torch.tensor(img.reshape(R, 3), dtype=torch.float32, device=dev)
-
-    poses, gts = map(list, zip(*[view() for _ in range(n_views)]))
-    ray_parts = 8 if args.config == "c5" else 1
-    views_per_step = 50 if args.config == "c4" else 1
-    if args.config == "c4":
-        # src/optimizer.py:66-98: codes only (weights fixed), every target view
-        # accumulates into the code gradients, then one AdamW step on the codes
-        from codenerf_amd.optim import FusedAdamW
-        from codenerf_amd.render import ImageStep
-        from codenerf_amd import engine as _eng
-        img = ImageStep(model, chunk=2048, reg_coef=1e-4, timers=timers)
-        sc1 = torch.nn.Parameter(shape_codes.detach()[:1].clone())
-        tc1 = torch.nn.Parameter(texture_codes.detach()[:1].clone())
-        copt = FusedAdamW([{"params": [sc1], "lr": 1e-2}, {"params": [tc1], "lr": 1e-2}])
-        extra = [view() for _ in range(50 - n_views)]
-        poses += [e[0] for e in extra]
-        gts += [e[1] for e in extra]
-
-    last = {}
-
-    def step(i):
-        if args.config == "c4":
-            sc1.grad = torch.zeros_like(sc1)
-            tc1.grad = torch.zeros_like(tc1)
-            for v in range(views_per_step):
-                ro, vd = _eng.get_rays_dev(H, W, focal, True, poses[v])
-                loss, _, _ = img.forward_backward(ro, vd, core.stratified_z(dev), gts[v], sc1, tc1, 0,
-                                                  weight_grads=False)
-                last.setdefault("views", []).append(loss)
-            copt.step()
-            last["losses"] = torch.cat(last.pop("views"))
-            return
-        v = i % n_views
-        obj = object_for(i, rank, world, n_obj)
-        last["losses"] = core.train_step(H, W, focal, poses[v], gts[v], obj, ray_parts=ray_parts)[0]
-
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    timers.on = True
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    samples_per_step = R * (args.n_coarse + args.n_fine) * views_per_step
+    wl = build_workload(args, dev, rank, world, args.precision, timers, dist)
+    dt, median = timed_run(wl, args.steps, args.warmup, timers, dist, dev)
+    samples_per_step = wl["samples_per_step"]
     value = samples_per_step * world * args.steps / dt
     ms = dt / args.steps * 1e3
 
     # train PSNR of the last timed step (src/trainer.py:99: -10 log10 of the
     # mean of the chunk MSEs; the fine pass's losses when n_fine > 0)
-    ls = last["losses"]
+    ls = wl["last"]["losses"]
     ls = ls[1] if isinstance(ls, tuple) else ls
     train_psnr = float(-10 * torch.log10(ls.float().mean()))
     if dist is not None:
@@ -230,75 +254,90 @@ def main():
         dist.all_reduce(t)
         train_psnr = float(t.item()) / world
 
-    summ = timers.summary()
-    kern = {k: v[0] for k, v in summ.items()}                     # ms per launch
-    per_step = {k: v[1] / args.steps for k, v in summ.items()}    # ms per step (all launches)
-    peak = BF16_PEAK_TFLOPS if args.precision == "bf16" else FP32_PEAK_TFLOPS
-    roof = None
-    if kern:
-        flops = {k: FLOP_PER_SAMPLE[k] * samples_per_step for k in FLOP_PER_SAMPLE if k in kern}
-        if args.config == "c4":
-            flops.pop("dw", None)       # codes-only: the dw timer brackets the bias sums
-        overlapped = args.n_fine > 0 and core.step_impl.overlap_dw
-        if overlapped:
-            # the dX chain of the coarse rows and dW of the fine rows run
-            # concurrently on two streams, so the phase spans overlap and the
-            # longest span is not the limiter: report the dW launches (the
-            # HBM-bound operand stream that bounds this design),
-            # each timed from the moment its rows are ready to its end
-            dom = "dw"
-        else:
-            dom = max(flops, key=lambda k: per_step[k])
-        # algorithmic FLOPs of the phase per step / its launch time per step
-        achieved = flops[dom] / (per_step[dom] * 1e-3) / 1e12
-        roof = {"bound": "mfma", "kernel": {"fwd": "chain_kernel<fwd,train>", "bwd": "chain_kernel<bwd>",
-                                            "dw": "dw_kernel"}[dom],
-                "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4), "traffic": load_traffic(args.config, dom),
-                "ms_per_launch": {k: round(v, 4) for k, v in kern.items()},
-                "ms_per_step_by_phase": {k: round(v, 4) for k, v in per_step.items()}}
-        if overlapped:
-            roof["overlap"] = ("2 dX + 2 dW launches per step: dX(fine rows); dX(coarse rows) || dW(fine rows) "
-                               "on a second stream; dW(coarse rows); phase spans overlap")
-        if dom == "dw" and args.precision == "bf16":
-            # the weight-gradient pass streams the stored bf16 operands (dA and X
-            # planes, 8,000 B per sample at the srncar net): its practical limiter
-            dw_bytes = DW_BYTES_PER_SAMPLE * samples_per_step
-            gbs = dw_bytes / (per_step["dw"] * 1e-3) / 1e9
-            roof["hbm_view"] = {"bytes_per_launch": dw_bytes, "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
-                                "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
-        step_flops = sum(v for k, v in FLOP_PER_SAMPLE.items() if args.config != "c4" or k != "dw") * samples_per_step
-        roof["step"] = {"achieved": round(step_flops / (ms * 1e-3) / 1e12, 2), "unit": "TFLOP/s",
-                        "frac": round(step_flops / (ms * 1e-3) / 1e12 / peak, 4)}
+    roof = roofline(args, timers, samples_per_step, ms, wl["core"].step_impl.overlap_dw)
+
+    # the reference's own precision on the same C2 geometry (secondary figure)
+    fp32 = None
+    if args.config in ("c2", "c3") and args.precision == "bf16" and not args.no_fp32:
+        t32 = Timers()
+        wl32 = build_workload(args, dev, rank, world, "fp32", t32, dist)
+        n32 = max(5, args.steps // 5)
+        dt32, med32 = timed_run(wl32, n32, 3, t32, dist, dev)
+        fp32 = {"value": round(samples_per_step * world * n32 / dt32, 1), "unit": "ray-samples/s",
+                "ms_per_step": round(dt32 / n32 * 1e3, 3), "ms_per_step_median": round(med32, 3), "steps": n32,
+                "dtype": "fp32"}
+        del wl32
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_threads)
+        cpu = cpu_baseline(args.cpu_threads, args)
 
     if rank == 0:
         metric = {"c2": "ray-samples/sec (train step), SRN-cars 128x128, 64 coarse + 64 fine samples",
                   "c4": "ray-samples/sec (optimize.py code optimisation step), 50 views x 128x128 x 64 samples",
                   "c3": "ray-samples/sec (train step), SRN-chairs geometry 128x128, 64 coarse + 64 fine samples",
                   "c5": "ray-samples/sec (train step), SRN-cars 256x256, 128 coarse + 128 fine samples, fp32"}
+        H = wl["H"]
         out = {
             "metric": metric[args.config],
             "value": round(value, 1), "unit": "ray-samples/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+            "warmup": args.warmup, "ms_per_step": round(ms, 3), "ms_per_step_median": round(median, 3),
+            "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
-            "data": f"synthetic ({H}x{W} ray-cast ellipsoid object per rank, poses on a radius-{radius} sphere, "
+            "data": f"synthetic ({H}x{H} ray-cast ellipsoid object per rank, poses on a radius-{wl['radius']} sphere, "
                     f"random-init weights)",
             "train_psnr": round(train_psnr, 3),
-            "config": {"workload": f"{'srnchair' if args.config == 'c3' else 'srncar'}.json net, {H}x{W} image/object/step, {args.n_coarse}+{args.n_fine} "
+            "config": {"workload": f"{'srnchair' if args.config == 'c3' else 'srncar'}.json net, {H}x{H} image/object/step, {args.n_coarse}+{args.n_fine} "
                                    f"samples/ray, " + ("50 views, codes-only fwd+dX+AdamW" if args.config == "c4"
                                                        else "train step incl. AdamW"),
                        "name": args.config, "objects_per_step": world,
-                       "rays_per_step_per_gpu": R, "parallelism": f"dp{world}"},
+                       "rays_per_step_per_gpu": wl["R"], "parallelism": f"dp{world}"},
             "roofline": roof,
+            "fp32": fp32,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()
+
+
+def roofline(args, timers, samples_per_step, ms, overlapped):
+    """Dominant kernel = the launch class with the most measured time per step
+    (HIP events on the stream each launch runs on); achieved = its
+    algorithmic FLOPs per step / that time."""
+    summ = timers.summary()
+    if not summ:
+        return None
+    kern = {k: v[0] for k, v in summ.items()}                     # ms per launch
+    per_step = {k: v[1] / args.steps for k, v in summ.items()}    # ms per step (all launches)
+    launches = {k: len(timers.ev[k]) / args.steps for k in timers.ev}
+    peak = BF16_PEAK_TFLOPS if args.precision == "bf16" else FP32_PEAK_TFLOPS
+    flops = {k: FLOP_PER_SAMPLE[k] * samples_per_step for k in FLOP_PER_SAMPLE if k in kern}
+    if args.config == "c4":
+        flops.pop("dw", None)       # codes-only: the dw timer brackets the bias sums
+    dom = max(flops, key=lambda k: per_step[k])
+    achieved = flops[dom] / (per_step[dom] * 1e-3) / 1e12
+    roof = {"bound": "mfma", "kernel": {"fwd": "chain_kernel<fwd,train>", "bwd": "chain_kernel<bwd>",
+                                        "dw": "dw_kernel"}[dom],
+            "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "traffic": load_traffic(args.config, dom),
+            "ms_per_launch": {k: round(v, 4) for k, v in kern.items()},
+            "launches_per_step": launches,
+            "ms_per_step_by_kernel": {k: round(v, 4) for k, v in per_step.items()}}
+    if overlapped and args.config != "c4":
+        roof["overlap"] = ("dX chain of row range i on the main stream || dW of range i-1 on a side stream; "
+                           "per-kernel spans overlap, so their sum exceeds the step")
+    if "dw" in per_step and args.precision == "bf16" and args.config != "c4":
+        # the weight-gradient pass streams the stored bf16 operands (dA and X
+        # planes, 8,000 B per sample at the srncar net): its HBM view
+        dw_bytes = DW_BYTES_PER_SAMPLE * samples_per_step
+        gbs = dw_bytes / (per_step["dw"] * 1e-3) / 1e9
+        roof["dw_hbm_view"] = {"bytes_per_step": dw_bytes, "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                               "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    step_flops = sum(v for k, v in FLOP_PER_SAMPLE.items() if args.config != "c4" or k != "dw") * samples_per_step
+    roof["step"] = {"achieved": round(step_flops / (ms * 1e-3) / 1e12, 2), "unit": "TFLOP/s",
+                    "frac": round(step_flops / (ms * 1e-3) / 1e12 / peak, 4)}
+    return roof
 
 
 def load_traffic(config, kernel):
@@ -312,28 +351,55 @@ def load_traffic(config, kernel):
         return None
 
 
-def cpu_baseline(threads):
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(threads, args):
     """The CPU oracle (torch fp32 restatement of the reference, pinned to its
-    golden vectors) on a bounded sample: a 2048-ray chunk x 128 samples,
-    forward + compositing + MSE + backward, timed on this host's cores."""
+    golden vectors) on a bounded sample of the SAME step: 1024 rays x
+    (n_coarse stratified + n_fine importance) samples -- coarse forward,
+    sample_pdf, fine forward, merged composite, both chunk-mean MSEs + code
+    regulariser, backward -- then AdamW over the model and both code tables
+    (codes-only for c4), timed on this host's cores for ~10 s."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     from oracle import ref_cpu
     from oracle.params import make_params
+    if threads is None:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
     torch.set_num_threads(threads)
     p = ref_cpu.param_tensors(make_params(0))
-    s = (torch.randn(1, 256) / 11.3).requires_grad_()
-    t = (torch.randn(1, 256) / 11.3).requires_grad_()
-    B, N = 2048, 128
+    n_obj = args.objects
+    st = (torch.randn(n_obj, 256) / 11.3).requires_grad_()
+    tt = (torch.randn(n_obj, 256) / 11.3).requires_grad_()
+    B, Nc, Nf = 1024, args.n_coarse, args.n_fine
     ro = torch.zeros(B, 3) + torch.tensor([0.0, 0.4, 1.2])
     vd = torch.nn.functional.normalize(torch.randn(B, 3) * 0.2 + torch.tensor([0., -0.3, -1.]), dim=-1)
-    z = torch.linspace(0.8, 1.8, N)
+    z = ref_cpu.stratified_z(0.8, 1.8, Nc)
     gt = torch.rand(B, 3)
+    codes_only = args.config == "c4"
+    groups = [([st], 1e-3), ([tt], 1e-3)] if codes_only else [(list(p.values()), 1e-4), ([st], 1e-3), ([tt], 1e-3)]
+    opt = ref_cpu.AdamWRef(groups)
 
     def one():
-        xyz = ro[:, None, :] + vd[:, None, :] * z[:, None]
-        sig, rgb = ref_cpu.codenerf_forward(p, xyz, vd[:, None, :].expand(-1, N, -1), s, t)
-        col, _ = ref_cpu.volume_rendering(sig, rgb, z)
-        ((col - gt) ** 2).mean().backward()
+        for t in list(p.values()) + [st, tt]:
+            t.grad = None
+        if Nf:
+            with torch.no_grad():
+                xyz = ro[:, None, :] + vd[:, None, :] * z[:, None]
+                sig_c, _ = ref_cpu.codenerf_forward(p, xyz, vd[:, None, :].expand(-1, Nc, -1), st[0][None], tt[0][None])
+                z_f = ref_cpu.sample_pdf(sig_c[..., 0], z, torch.rand(B, Nf))
+            ref_cpu.fine_image_step(p, st, tt, 0, ro, vd, z, z_f, gt, chunk=B)
+        else:
+            ref_cpu.image_step(p, st, tt, 0, ro, vd, z, gt, chunk=B)
+        opt.step()
 
     one()
     reps, t0 = 0, time.perf_counter()
@@ -341,8 +407,13 @@ def cpu_baseline(threads):
         one()
         reps += 1
     dt = time.perf_counter() - t0
-    return {"value": round(B * N * reps / dt, 1), "unit": "ray-samples/s", "cores": threads, "kind": "port",
-            "sample": f"{reps} x (2048 rays x 128 samples) fwd+composite+MSE+backward, torch CPU fp32 oracle"}
+    what = "codes-only fwd+composite+MSE+backward+AdamW(codes)" if codes_only else \
+        ("coarse fwd + sample_pdf + fine fwd + merged composite + MSEs + backward + AdamW(model, code tables)"
+         if Nf else "fwd+composite+MSE+backward+AdamW")
+    return {"value": round(B * (Nc + Nf) * reps / dt, 1), "unit": "ray-samples/s", "cores": threads,
+            "host_cpus": os.cpu_count(), "cpu_model": cpu_model(), "kind": "port",
+            "sample": f"{reps} x ({B} rays x {Nc}+{Nf} samples) {what}, torch CPU fp32 oracle "
+                      f"(oracle/ref_cpu.py; the coarse forward runs twice, once without grad for sample_pdf), {threads} threads"}
 
 
 if __name__ == "__main__":

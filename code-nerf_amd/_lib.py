@@ -15,6 +15,7 @@ LIB_NAME = "libcodenerf_hip.so"
 # built side by side for A/B measurements); it must export the same ABI.
 LIB_PATH = os.environ.get("CODENERF_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
+ABI_VERSION = 2
 CN_FP32 = 0
 CN_BF16 = 1
 
@@ -41,6 +42,8 @@ _SIGS = {
     "cn_plan_num_params": (_I, [_P]),
     "cn_plan_num_inject": (_I, [_P]),
     "cn_pad_samples": (_I, [_P, _I]),
+    "cn_max_samples": (_I, []),
+    "cn_act_bytes_per_sample": (_Z, [_P]),
     "cn_packed_bytes": (_Z, [_P, _I]),
     "cn_blob_floats": (_Z, [_P]),
     "cn_act_bytes": (_Z, [_P, _I]),
@@ -50,11 +53,11 @@ _SIGS = {
     "cn_mlp_fwd": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _I, _I, _P]),
     "cn_mlp_bwd": (_I, [_P, _P, _P, _I, _P, _P, _P, _P]),
     "cn_mlp_fwd_codes": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _I, _I, _P]),
-    "cn_mlp_bwd_codes": (_I, [_P, _P, _P, _I, _P, _P, _P, _P]),
+    "cn_mlp_bwd_codes": (_I, [_P, _P, _P, _I, _P, _P, _P, _I, _I, _P]),
     "cn_mlp_dw": (_I, [_P, _P, _I, _P, _P, _P, _P, _P]),
     "cn_mlp_bwd_rows": (_I, [_P, _P, _P, _I, _P, _P, _P, _I, _I, _P]),
-    "cn_mlp_dw_rows": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _I, _P, _P]),
-    "cn_mlp_dbias": (_I, [_P, _P, _I, _P, _P, _P]),
+    "cn_mlp_dw_rows": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _I, _I, _P, _P]),
+    "cn_mlp_dbias": (_I, [_P, _P, _I, _I, _P, _P, _P]),
     "cn_latent_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P]),
     "cn_get_rays": (_I, [_I, _I, _D, _I, _P, _P, _P, _P]),
     "cn_sample_points": (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P]),
@@ -80,7 +83,7 @@ def load_library(path=LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.cn_abi_version() != 1:
+    if lib.cn_abi_version() != ABI_VERSION:
         raise HipUnavailable("libcodenerf_hip.so ABI version mismatch")
     return lib
 

@@ -2,6 +2,7 @@
 #include <stdio.h>
 #include <string.h>
 #include <algorithm>
+#include <mutex>
 #include <cmath>
 #include <string>
 #include <vector>
@@ -17,9 +18,14 @@ using namespace cn;
 
 struct cn_plan {
   ChainSet cs;
+  // packing tables (host), uploaded to the device by the first cn_pack_weights
+  // so that creating a plan and querying sizes / validating arguments needs no
+  // device
+  std::vector<int32_t> h_fwd_idx, h_bwd_idx;
   int32_t* d_fwd_idx = nullptr;
   int32_t* d_bwd_idx = nullptr;
   int fwd_n = 0, bwd_n = 0;
+  std::mutex upload_mu;
 };
 
 namespace {
@@ -56,18 +62,40 @@ int cn_plan_create(int shape_blocks, int texture_blocks, int W, int num_xyz_freq
   else return fail("cn_plan_create: unsupported (shape_blocks, texture_blocks); built: (3,1), (2,1)");
   cn_plan* p = new cn_plan();
   p->cs = cs;
-  std::vector<int32_t> tf = cs.fwd_table(), tb = cs.bwd_table();
-  p->fwd_n = (int)tf.size();
-  p->bwd_n = (int)tb.size();
-  if (check(hipMalloc(&p->d_fwd_idx, tf.size() * 4), "hipMalloc") ||
-      check(hipMalloc(&p->d_bwd_idx, tb.size() * 4), "hipMalloc") ||
-      check(hipMemcpy(p->d_fwd_idx, tf.data(), tf.size() * 4, hipMemcpyHostToDevice), "hipMemcpy") ||
-      check(hipMemcpy(p->d_bwd_idx, tb.data(), tb.size() * 4, hipMemcpyHostToDevice), "hipMemcpy")) {
-    std::string e = g_err;
-    cn_plan_destroy(p);
-    return fail(e);
-  }
+  p->h_fwd_idx = cs.fwd_table();
+  p->h_bwd_idx = cs.bwd_table();
+  p->fwd_n = (int)p->h_fwd_idx.size();
+  p->bwd_n = (int)p->h_bwd_idx.size();
   *out = p;
+  return 0;
+}
+
+static int upload_tables(cn_plan* p) {
+  std::lock_guard<std::mutex> lk(p->upload_mu);
+  if (p->d_fwd_idx) return 0;
+  int32_t *f = nullptr, *b = nullptr;
+  if (check(hipMalloc(&f, p->h_fwd_idx.size() * 4), "hipMalloc") ||
+      check(hipMalloc(&b, p->h_bwd_idx.size() * 4), "hipMalloc") ||
+      check(hipMemcpy(f, p->h_fwd_idx.data(), p->h_fwd_idx.size() * 4, hipMemcpyHostToDevice), "hipMemcpy") ||
+      check(hipMemcpy(b, p->h_bwd_idx.data(), p->h_bwd_idx.size() * 4, hipMemcpyHostToDevice), "hipMemcpy")) {
+    if (f) (void)hipFree(f);
+    if (b) (void)hipFree(b);
+    return -1;
+  }
+  p->d_bwd_idx = b;
+  p->d_fwd_idx = f;
+  return 0;
+}
+
+// Sample-count guard shared by every per-sample entry point: sample indices
+// (3 m, 4 m) are 32-bit in the kernels.  The activation planes themselves
+// have no size limit (each wave addresses its own slab through a 64-bit
+// descriptor base, chain.hip slab_rsrc).
+static int check_samples(long long M, const char* who) {
+  if (M <= 0) return fail(std::string(who) + ": M must be positive");
+  if (M > CN_MAX_SAMPLES)
+    return fail(std::string(who) + ": " + std::to_string(M) + " samples exceed CN_MAX_SAMPLES (" +
+                std::to_string((long long)CN_MAX_SAMPLES) + ") per call; split the rays into parts");
   return 0;
 }
 
@@ -80,14 +108,23 @@ void cn_plan_destroy(cn_plan* p) {
 
 int cn_plan_num_params(const cn_plan* p) { return p ? p->cs.n_params : -1; }
 int cn_plan_num_inject(const cn_plan* p) { return p ? p->cs.n_inject : -1; }
-int cn_pad_samples(const cn_plan* p, int M) { return p ? ((M + 255) / 256) * 256 : -1; }
+int cn_pad_samples(const cn_plan* p, int M) {
+  return p && M >= 0 && M <= CN_MAX_SAMPLES ? ((M + 255) / 256) * 256 : -1;
+}
+int cn_max_samples(void) { return CN_MAX_SAMPLES; }
 size_t cn_packed_bytes(const cn_plan* p, int bwd) { return p ? (bwd ? p->cs.pack_bwd_bytes : p->cs.pack_fwd_bytes) : 0; }
 size_t cn_blob_floats(const cn_plan* p) { return p ? (size_t)p->cs.blob_floats : 0; }
-size_t cn_act_bytes(const cn_plan* p, int M) { return p ? p->cs.layout(cn_pad_samples(p, M)).bytes : 0; }
+size_t cn_act_bytes(const cn_plan* p, int M) {
+  return p && M > 0 && M <= CN_MAX_SAMPLES ? p->cs.layout(cn_pad_samples(p, M)).bytes : 0;
+}
+size_t cn_act_bytes_per_sample(const cn_plan* p) {
+  return p ? p->cs.layout(1 << 20).bytes >> 20 : 0;
+}
 size_t cn_dw_ws_bytes(const cn_plan* p, int M) { return p ? p->cs.dw_ws_bytes(M) : 0; }
 
 int cn_pack_weights(const cn_plan* p, const float* const* d_params, void* d_fwd, void* d_bwd, void* stream) {
   if (!p || !d_params) return fail("cn_pack_weights: NULL argument");
+  if (!p->d_fwd_idx && upload_tables(const_cast<cn_plan*>(p))) return -1;
   const int bf16 = p->cs.prec;
   if (d_fwd) {
     hipLaunchKernelGGL(pack_kernel, dim3(grid_for(p->fwd_n, 256)), dim3(256), 0, S(stream), d_params,
@@ -116,7 +153,7 @@ static int mlp_fwd_impl(int codes, const cn_plan* p, const void* d_pack, const f
                         int act_M, int act_row0, void* stream) {
   if (codes && !d_act) return fail("cn_mlp_fwd_codes: the activation workspace is required");
   if (!p || !d_pack || !d_blob || !d_sigma || !d_rgb) return fail("cn_mlp_fwd: NULL argument");
-  if (M <= 0) return fail("cn_mlp_fwd: M must be positive");
+  if (check_samples(M, "cn_mlp_fwd")) return -1;
   ChainArgs a{};
   a.wpack = d_pack;
   a.bias = d_blob;
@@ -146,6 +183,7 @@ static int mlp_fwd_impl(int codes, const cn_plan* p, const void* d_pack, const f
     // [act_row0, act_row0 + Mp) of it (coarse and fine passes share one
     // workspace, so one backward / dW covers both)
     if (act_M <= 0) act_M = M;
+    if (check_samples(act_M, "cn_mlp_fwd (act_M)")) return -1;
     if (act_row0 < 0 || act_row0 % p->cs.tile) return fail("cn_mlp_fwd: act_row0 must be a multiple of the tile");
     const int Ma = cn_pad_samples(p, act_M);
     if (act_row0 + Mp > Ma) return fail("cn_mlp_fwd: rows exceed the activation workspace");
@@ -189,7 +227,7 @@ static int mlp_bwd_impl(int codes, const cn_plan* p, const void* d_pack, const f
                         const float* d_dsigma, const float* d_drgb, void* d_act, int act_M, int act_row0,
                         void* stream) {
   if (!p || !d_pack || !d_blob || !d_dsigma || !d_drgb || !d_act) return fail("cn_mlp_bwd: NULL argument");
-  if (M <= 0) return fail("cn_mlp_bwd: M must be positive");
+  if (check_samples(M, "cn_mlp_bwd")) return -1;
   ChainArgs a{};
   a.wpack = d_pack;
   a.bias = d_blob;
@@ -199,6 +237,7 @@ static int mlp_bwd_impl(int codes, const cn_plan* p, const void* d_pack, const f
   const int Mp = cn_pad_samples(p, M);
   // rows [act_row0, act_row0 + Mp) of a workspace laid out for act_M samples
   if (act_M <= 0) act_M = M;
+  if (check_samples(act_M, "cn_mlp_bwd (act_M)")) return -1;
   if (act_row0 < 0 || act_row0 % p->cs.tile) return fail("cn_mlp_bwd: act_row0 must be a multiple of the tile");
   const int Ma = cn_pad_samples(p, act_M);
   if (act_row0 + Mp > Ma) return fail("cn_mlp_bwd: rows exceed the activation workspace");
@@ -231,21 +270,23 @@ int cn_mlp_bwd_rows(const cn_plan* p, const void* d_pack, const float* d_blob, i
 }
 
 int cn_mlp_bwd_codes(const cn_plan* p, const void* d_pack, const float* d_blob, int M, const float* d_dsigma,
-                     const float* d_drgb, void* d_act, void* stream) {
-  return mlp_bwd_impl(1, p, d_pack, d_blob, M, d_dsigma, d_drgb, d_act, M, 0, stream);
+                     const float* d_drgb, void* d_act, int act_M, int act_row0, void* stream) {
+  return mlp_bwd_impl(1, p, d_pack, d_blob, M, d_dsigma, d_drgb, d_act, act_M, act_row0, stream);
 }
 
 static int mlp_dw_impl(const cn_plan* p, void* d_act, int act_M, int act_row0, int M, const float* d_zvec,
-                       float* const* d_grads, float* d_dbuf, int db_accum, void* d_ws, void* stream) {
+                       float* const* d_grads, float* d_dbuf, int db_accum, int nwg_req, void* d_ws, void* stream) {
   if (!p || !d_act || !d_zvec || !d_grads || !d_dbuf || !d_ws) return fail("cn_mlp_dw: NULL argument");
-  if (M <= 0) return fail("cn_mlp_dw: M must be positive");
+  if (check_samples(M, "cn_mlp_dw")) return -1;
   if (act_M <= 0) act_M = M;
+  if (check_samples(act_M, "cn_mlp_dw (act_M)")) return -1;
   if (act_row0 < 0 || act_row0 % 256 || act_row0 + cn_pad_samples(p, M) > cn_pad_samples(p, act_M))
     return fail("cn_mlp_dw: rows exceed the activation workspace (act_row0 must be a multiple of 256)");
   DwArgs dw;
   DwRedArgs red;
-  const int nwg = p->cs.dw_setup((char*)d_act, act_M, act_row0, M, d_zvec, d_dbuf, (char*)d_ws, &dw, &red);
-  if (nwg <= 0) return fail("cn_mlp_dw: schedule does not fit the partial workspace");
+  if (nwg_req < 0 || nwg_req > 256) return fail("cn_mlp_dw_rows: n_workgroups must be in [0, 256]");
+  const int nwg = p->cs.dw_setup((char*)d_act, act_M, act_row0, M, nwg_req, d_zvec, d_dbuf, (char*)d_ws, &dw, &red);
+  if (nwg <= 0) return fail("cn_mlp_dw: schedule does not fit (too few workgroups for the layer sizes?)");
   red.grads = d_grads;
   red.db_accum = db_accum ? 1 : 0;
   if (p->cs.prec) hipLaunchKernelGGL(dw_kernel<CN_P_BF16>, dim3(nwg), dim3(512), 0, S(stream), dw);
@@ -257,19 +298,23 @@ static int mlp_dw_impl(const cn_plan* p, void* d_act, int act_M, int act_row0, i
 
 int cn_mlp_dw(const cn_plan* p, void* d_act, int M, const float* d_zvec, float* const* d_grads, float* d_dbuf,
               void* d_ws, void* stream) {
-  return mlp_dw_impl(p, d_act, M, 0, M, d_zvec, d_grads, d_dbuf, 0, d_ws, stream);
+  return mlp_dw_impl(p, d_act, M, 0, M, d_zvec, d_grads, d_dbuf, 0, 0, d_ws, stream);
 }
 
 int cn_mlp_dw_rows(const cn_plan* p, void* d_act, int act_M, int act_row0, int M, const float* d_zvec,
-                   float* const* d_grads, float* d_dbuf, int db_accum, void* d_ws, void* stream) {
-  return mlp_dw_impl(p, d_act, act_M, act_row0, M, d_zvec, d_grads, d_dbuf, db_accum, d_ws, stream);
+                   float* const* d_grads, float* d_dbuf, int db_accum, int n_workgroups, void* d_ws,
+                   void* stream) {
+  return mlp_dw_impl(p, d_act, act_M, act_row0, M, d_zvec, d_grads, d_dbuf, db_accum, n_workgroups, d_ws, stream);
 }
 
-int cn_mlp_dbias(const cn_plan* p, void* d_act, int M, float* d_dbuf, void* d_ws, void* stream) {
+int cn_mlp_dbias(const cn_plan* p, void* d_act, int act_M, int M, float* d_dbuf, void* d_ws, void* stream) {
   if (!p || !d_act || !d_dbuf || !d_ws) return fail("cn_mlp_dbias: NULL argument");
-  if (M <= 0) return fail("cn_mlp_dbias: M must be positive");
+  if (check_samples(M, "cn_mlp_dbias")) return -1;
+  if (act_M <= 0) act_M = M;
+  if (check_samples(act_M, "cn_mlp_dbias (act_M)")) return -1;
   DbArgs db;
-  if (p->cs.db_setup((char*)d_act, M, d_dbuf, (char*)d_ws, &db) < 0) return fail("cn_mlp_dbias: unsupported plane width");
+  if (p->cs.db_setup((char*)d_act, act_M, M, d_dbuf, (char*)d_ws, &db) < 0)
+    return fail("cn_mlp_dbias: rows exceed the workspace or unsupported plane width");
   if (db.ninj <= 0) return 0;
   if (p->cs.prec) hipLaunchKernelGGL(db_kernel<CN_P_BF16>, dim3(kDbBlocks, db.ninj), dim3(256), 0, S(stream), db);
   else hipLaunchKernelGGL(db_kernel<CN_P_FP32>, dim3(kDbBlocks, db.ninj), dim3(256), 0, S(stream), db);
@@ -293,6 +338,7 @@ int cn_latent_bwd(const cn_plan* p, const float* const* d_params, float* const* 
 int cn_get_rays(int H, int W, double focal, int focal_is_f64, const float* d_c2w, float* d_ro, float* d_vd,
                 void* stream) {
   if (!d_c2w || !d_ro || !d_vd || H <= 0 || W <= 0) return fail("cn_get_rays: bad argument");
+  if (check_samples((long long)H * W, "cn_get_rays")) return -1;
   hipLaunchKernelGGL(get_rays_kernel, dim3(grid_for((long)H * W, 256)), dim3(256), 0, S(stream), H, W, focal,
                      focal_is_f64, d_c2w, d_ro, d_vd);
   return launch_check("get_rays_kernel");
@@ -301,6 +347,7 @@ int cn_get_rays(int H, int W, double focal, int focal_is_f64, const float* d_c2w
 int cn_sample_points(const float* d_ro, const float* d_vd, const float* d_z, int z_stride, int R, int N,
                      float* d_xyz, float* d_vrep, void* stream) {
   if (!d_ro || !d_vd || !d_z || !d_xyz || !d_vrep || R <= 0 || N <= 0) return fail("cn_sample_points: bad argument");
+  if (check_samples((long long)R * N, "cn_sample_points")) return -1;
   hipLaunchKernelGGL(stratified_points_kernel, dim3(grid_for((long)R * N, 256)), dim3(256), 0, S(stream), d_ro,
                      d_vd, d_z, z_stride, R, N, d_xyz, d_vrep);
   return launch_check("stratified_points_kernel");
@@ -309,6 +356,7 @@ int cn_sample_points(const float* d_ro, const float* d_vd, const float* d_z, int
 static int check_rn(int R, int N, const char* who) {
   if (R <= 0 || N <= 0) return fail(std::string(who) + ": R and N must be positive");
   if (N > 64 * kMaxPer) return fail(std::string(who) + ": at most 256 samples per ray");
+  if (check_samples((long long)R * N, who)) return -1;
   return 0;
 }
 

@@ -83,10 +83,17 @@ CN_DEV uint32_t push_sign(uint32_t bits, float v) {
 // lane's sample into the wave-tiled plane layout (cn_layout.h): the per-lane
 // part of the address is voff[g] (precomputed), the rest is wave-uniform.
 template <class E>
-CN_DEV void plane_store(__amdgpu_buffer_rsrc_t r, const uint32_t* voff, int F, int wglob, int t, int g,
+CN_DEV void plane_store(__amdgpu_buffer_rsrc_t r, const uint32_t* voff, int t, int g,
                         float a, float b, float c, float d) {
-  const int soff = (wglob * (F >> 5) + t) * (1024 * (int)sizeof(E));
-  bstore4<E>(r, voff[g], soff, a, b, c, d);
+  bstore4<E>(r, voff[g], t * (1024 * (int)sizeof(E)), a, b, c, d);
+}
+// Buffer descriptor of wave wglob's 32-sample slab of a plane of width F: the
+// 64-bit slab base is wave-uniform (scalar arithmetic) and goes into the
+// descriptor, so every per-store offset stays below one slab (<= 36 KiB).  No
+// 4 GB descriptor range or 32-bit offset bounds the plane size.
+template <class E>
+CN_DEV __amdgpu_buffer_rsrc_t slab_rsrc(const void* plane, int F, int wglob) {
+  return mkrsrc((const char*)plane + (size_t)wglob * (size_t)F * 32u * sizeof(E));
 }
 // bf16: groups 2gp and 2gp+1 of feature tile t (this lane: 4 + 4 features as
 // packed pairs) -> one 16-B store per lane.  v_permlane32_swap exchanges the
@@ -101,12 +108,12 @@ CN_DEV void plane_store(__amdgpu_buffer_rsrc_t r, const uint32_t* voff, int F, i
 // rewritten that register.  The data therefore passes through an asm
 // barrier with wait states before the store, and stays live through a second
 // one after it, so no VALU can reuse those registers inside the window.
-CN_DEV void plane_store_pair(__amdgpu_buffer_rsrc_t r, uint32_t voff16, int F, int wglob, int t, u32x2 a, u32x2 b) {
+CN_DEV void plane_store_pair(__amdgpu_buffer_rsrc_t r, uint32_t voff16, int t, u32x2 a, u32x2 b) {
   const auto x = __builtin_amdgcn_permlane32_swap(a[0], b[0], false, false);
   const auto y = __builtin_amdgcn_permlane32_swap(a[1], b[1], false, false);
   u32x4 d = u32x4{x[0], y[0], x[1], y[1]};
   asm volatile("s_nop 3" : "+v"(d));
-  bstore128(r, voff16, d, (wglob * (F >> 5) + t) * 2048);
+  bstore128(r, voff16, d, t * 2048);
   asm volatile("s_nop 1" ::"v"(d) : "memory");
 }
 
@@ -290,7 +297,7 @@ struct Chain {
             constexpr int plane = S::L(pl).plane;
             constexpr int F = BWD ? N::dplane_width(plane) : N::plane_width(plane);
             const u32x4 b = bin[j];                    // tile j / 2, pair j % 2
-            plane_store_pair(mkrsrc(BWD ? a.dA[plane] : a.Y[plane]), voff[4 + (j & 1)], F, wglob, j >> 1,
+            plane_store_pair(slab_rsrc<E>(BWD ? a.dA[plane] : a.Y[plane], F, wglob), voff[4 + (j & 1)], j >> 1,
                              u32x2{b[0], b[1]}, u32x2{b[2], b[3]});
           }
         }
@@ -400,14 +407,14 @@ struct Chain {
     if constexpr (PLANES) {
       // slot q of lane half h -> column slot_col(h, q): group k = q / 4 lands in
       // feature tile k / 4, group k % 4 (cn_layout.h)
-      const auto rp = mkrsrc(a.pe);
+      const auto rp = slab_rsrc<E>(a.pe, 64, wglob);
 #pragma unroll
       for (int k = 0; k < 8; ++k)
-        plane_store<E>(rp, voff, 64, wglob, k >> 2, k & 3, pe[4 * k], pe[4 * k + 1], pe[4 * k + 2], pe[4 * k + 3]);
-      const auto rd = mkrsrc(a.dir);
+        plane_store<E>(rp, voff, k >> 2, k & 3, pe[4 * k], pe[4 * k + 1], pe[4 * k + 2], pe[4 * k + 3]);
+      const auto rd = slab_rsrc<E>(a.dir, 32, wglob);
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        plane_store<E>(rd, voff, 32, wglob, 0, k, dp[4 * k], dp[4 * k + 1], dp[4 * k + 2], dp[4 * k + 3]);
+        plane_store<E>(rd, voff, 0, k, dp[4 * k], dp[4 * k + 1], dp[4 * k + 2], dp[4 * k + 3]);
     }
   }
 
@@ -434,18 +441,18 @@ struct Chain {
     if constexpr (PLANES) {
       // drgb as a padded 32-wide plane for the rgb-head weight gradient
       // (columns slot_col(0, 0..2) = 0..2)
-      const auto r8 = mkrsrc(a.d8);
-      plane_store<E>(r8, voff, 32, wglob, 0, 0, h ? 0.f : g0, h ? 0.f : g1, h ? 0.f : g2, 0.f);
+      const auto r8 = slab_rsrc<E>(a.d8, 32, wglob);
+      plane_store<E>(r8, voff, 0, 0, h ? 0.f : g0, h ? 0.f : g1, h ? 0.f : g2, 0.f);
 #pragma unroll
-      for (int k = 1; k < 4; ++k) plane_store<E>(r8, voff, 32, wglob, 0, k, 0.f, 0.f, 0.f, 0.f);
+      for (int k = 1; k < 4; ++k) plane_store<E>(r8, voff, 0, k, 0.f, 0.f, 0.f, 0.f);
       // the sigma-head gradient rides in columns 256 (value) and 257 (its
       // rounding residual, so bf16 storage keeps ~16 significant bits) of the
       // viewdir dA plane (feature tile 8 of its 288 columns)
-      const auto rv = mkrsrc(a.dA[SB + 2]);
+      const auto rv = slab_rsrc<E>(a.dA[SB + 2], 288, wglob);
       const float ds_hi = (float)(E)ds;
-      plane_store<E>(rv, voff, 288, wglob, 8, 0, h ? 0.f : ds_hi, h ? 0.f : ds - ds_hi, 0.f, 0.f);
+      plane_store<E>(rv, voff, 8, 0, h ? 0.f : ds_hi, h ? 0.f : ds - ds_hi, 0.f, 0.f);
 #pragma unroll
-      for (int k = 1; k < 4; ++k) plane_store<E>(rv, voff, 288, wglob, 8, k, 0.f, 0.f, 0.f, 0.f);
+      for (int k = 1; k < 4; ++k) plane_store<E>(rv, voff, 8, k, 0.f, 0.f, 0.f, 0.f);
     }
     // ReLU sign bits of this wave -> LDS
     const u32x4* src = (const u32x4*)a.masks + (size_t)wglob * N::kMasks * 64 + lane;
@@ -472,7 +479,7 @@ struct Chain {
       uint32_t mbits[4] = {0u, 0u, 0u, 0u};
       constexpr int yp = l.plane >= 0 ? l.plane : 0;
       constexpr int YF = N::plane_width(yp);
-      const auto ry = mkrsrc(a.Y[yp]);
+      const auto ry = slab_rsrc<E>(a.Y[yp], YF, wglob);
       const float* ws = prm + kWsOff + 4 * h;
 #pragma unroll
       for (int t = 0; t < l.T; ++t) {
@@ -501,7 +508,7 @@ struct Chain {
             if ((g & 1) == 0) { b[0] = p0; b[1] = p1; } else { b[2] = p0; b[3] = p1; }
             pg[g] = u32x2{p0, p1};
             if constexpr (plane_of(LI) && !defers(LI))
-              if (g & 1) plane_store_pair(ry, voff[4 + (g >> 1)], YF, wglob, t, pg[g - 1], pg[g]);
+              if (g & 1) plane_store_pair(ry, voff[4 + (g >> 1)], t, pg[g - 1], pg[g]);
           } else {
             if constexpr (l.epi == EPI_RELU) {
               v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
@@ -511,12 +518,12 @@ struct Chain {
             bin[16 * t + 4 * g + 2] = v2;
             bin[16 * t + 4 * g + 3] = v3;
             if constexpr (plane_of(LI))
-              plane_store<E>(ry, voff, YF, wglob, t, g, v0, v1, v2, v3);
+              plane_store<E>(ry, voff, t, g, v0, v1, v2, v3);
           }
         }
       }
       if constexpr (TRAIN && l.mask >= 0) {
-        bstore128(mkrsrc(a.masks), (((uint32_t)wglob * N::kMasks + l.mask) * 64 + lane) * 16,
+        bstore128(mkrsrc(a.masks + (size_t)wglob * N::kMasks * 256), ((uint32_t)l.mask * 64 + lane) * 16,
                   u32x4{mbits[0], mbits[1], mbits[2], mbits[3]});
       }
       if constexpr (l.epi == EPI_SHAPE) {
@@ -556,7 +563,7 @@ struct Chain {
                                       const uint32_t* voff, float ds) {
     constexpr Layer l = S::L(LI);
     constexpr int width = N::dplane_width(l.plane);
-    const auto rdA = mkrsrc(a.dA[l.plane]);
+    const auto rdA = slab_rsrc<E>(a.dA[l.plane], width, wglob);
     u32x4 mw = u32x4{0u, 0u, 0u, 0u};
     if constexpr (l.epi == EPI_BMASK)
       mw = *(const u32x4*)(smem + kMaskOff + (((size_t)w * N::kMasks + l.mask) * 64 + lane) * 16);
@@ -593,11 +600,11 @@ struct Chain {
           if ((g & 1) == 0) { b[0] = p0; b[1] = p1; } else { b[2] = p0; b[3] = p1; }
           pg[g] = u32x2{p0, p1};
           if constexpr (plane_of(LI) && !defers(LI))
-            if (g & 1) plane_store_pair(rdA, voff[4 + (g >> 1)], width, wglob, t, pg[g - 1], pg[g]);
+            if (g & 1) plane_store_pair(rdA, voff[4 + (g >> 1)], t, pg[g - 1], pg[g]);
         } else {
 #pragma unroll
           for (int i = 0; i < 4; ++i) bin[16 * t + 4 * g + i] = v[i];
-          if constexpr (plane_of(LI)) plane_store<E>(rdA, voff, width, wglob, t, g, v[0], v[1], v[2], v[3]);
+          if constexpr (plane_of(LI)) plane_store<E>(rdA, voff, t, g, v[0], v[1], v[2], v[3]);
         }
       }
       acc[t] = f32x16{};

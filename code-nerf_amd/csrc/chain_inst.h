@@ -39,11 +39,11 @@ struct ChainSet {
   std::vector<int32_t> (*bwd_table)() = nullptr;
   ActLayout (*layout)(size_t Mp) = nullptr;
   // fills the dW / reduce argument blocks; returns the number of dW workgroups
-  int (*dw_setup)(char* act, int act_M, int row0, int M, const float* zvec, float* dbuf, char* ws, DwArgs* dw,
-                  DwRedArgs* red) = nullptr;
+  int (*dw_setup)(char* act, int act_M, int row0, int M, int nwg, const float* zvec, float* dbuf, char* ws,
+                  DwArgs* dw, DwRedArgs* red) = nullptr;
   size_t (*dw_ws_bytes)(int M) = nullptr;
   // fills the bias-only argument block (dbuf rows of the injection layers)
-  int (*db_setup)(char* act, int M, float* dbuf, char* ws, DbArgs* db) = nullptr;
+  int (*db_setup)(char* act, int act_M, int M, float* dbuf, char* ws, DbArgs* db) = nullptr;
 };
 
 ChainSet chain_set_fp32_3_1();

@@ -97,8 +97,9 @@ ActLayout act_layout(size_t Mp) {
   return L;
 }
 
-// dW schedule for M samples: kDwWorkgroups persistent workgroups (one per CU)
-// each take an equal byte share of the (layer, slab) stream.
+// dW schedule for M samples: nwg persistent workgroups (default kDwWorkgroups,
+// one per CU) each take an equal byte share of the (layer, slab) stream.
+// Fewer workgroups leave CUs to a dX chain running beside the dW pass.
 constexpr int kDwWorkgroups = 256;
 
 template <int P, int SB, int TB>
@@ -110,8 +111,8 @@ size_t dw_ws_bytes(int) {
 // (row0 a multiple of 256): the coarse and fine row ranges of one step can
 // then be reduced by two launches, each overlapping the other range's dX chain.
 template <int P, int SB, int TB>
-int dw_setup(char* act, int act_M, int row0, int M, const float* zvec, float* dbuf, char* ws, DwArgs* dw,
-             DwRedArgs* red) {
+int dw_setup(char* act, int act_M, int row0, int M, int nwg_req, const float* zvec, float* dbuf, char* ws,
+             DwArgs* dw, DwRedArgs* red) {
   using N = Net<SB, TB>;
   constexpr ParamIdx PI{SB, TB};
   constexpr int ES = P == CN_P_BF16 ? 2 : 4;
@@ -175,7 +176,7 @@ int dw_setup(char* act, int act_M, int row0, int M, const float* zvec, float* db
   red->prefix[N::kFwdLayers] = ep;
   // a share (wsum / nwg bytes) never exceeds the smallest problem, so it
   // holds slabs of at most two problems
-  const long long nwg = kDwWorkgroups;
+  const long long nwg = nwg_req > 0 ? std::min(nwg_req, kDwWorkgroups) : kDwWorkgroups;
   if ((wsum + min_total - 1) / min_total >= nwg) return -1;
   dw->nwg = red->nwg = (int)nwg;
   // which partial slots hold each problem (the kernel's own segment walk)
@@ -203,10 +204,13 @@ int dw_setup(char* act, int act_M, int row0, int M, const float* zvec, float* db
 }
 
 template <int P, int SB, int TB>
-int db_setup(char* act, int M, float* dbuf, char* ws, DbArgs* db) {
+int db_setup(char* act, int act_M, int M, float* dbuf, char* ws, DbArgs* db) {
+  // rows [0, pad(M)) of a workspace laid out for act_M samples
   using N = Net<SB, TB>;
   const int Mp = ((M + 255) / 256) * 256;
-  const ActLayout A = act_layout<P, SB, TB>(Mp);
+  const int Ma = ((act_M + 255) / 256) * 256;
+  if (Mp > Ma) return -1;
+  const ActLayout A = act_layout<P, SB, TB>(Ma);
   static_assert(N::kInject <= kDbMaxInject, "injections");
   *db = DbArgs{};
   db->total_slabs = Mp / 32;

@@ -1,17 +1,30 @@
 """Data-parallel plumbing of the training step.
 
 One process per GPU; each rank renders its own object(s) (weak scaling: the
-per-rank work is fixed as ranks are added).  The only exchange per optimiser
-step is one SUM all-reduce of the flat fp32 gradient bucket (RCCL over xGMI
-on MI355X; gloo in the CPU tests) -- model gradients (714,756 floats, 2.9 MB)
-followed by the two code tables, whose rows are touched only by the objects
-rendered this step.  Every rank then runs the same dense AdamW on identical
-data, so replicas stay bit-identical without a parameter broadcast.
+per-rank work is fixed as ranks are added).  Per optimiser step the ranks
+exchange
 
-The reference has no distributed path (one device, src/trainer.py:25); with
-one rank this reduces exactly to its loop.
+  * the model gradients: one SUM all-reduce of a flat fp32 bucket (714,756
+    floats = 2.86 MB at the srncar net; RCCL over xGMI on MI355X, gloo in the
+    CPU tests), issued asynchronously so the code-table exchange and the
+    code-table AdamW run while it is in flight;
+  * the code-table gradients, which are row-sparse (a rank touches only the
+    rows of the objects it rendered): an all_gather of (row index, shape row,
+    texture row) = 513 floats per rendered object, scattered back into the
+    dense gradient tables in rank order on every rank.
+
+Every rank then runs the same dense AdamW over the model and both code tables
+(the reference's dense-embedding AdamW moves every row every step,
+src/trainer.py:116-120), so replicas stay bit-identical without a parameter
+broadcast.  The reference has no distributed path (one device,
+src/trainer.py:25); with one rank every exchange is skipped and the step is
+exactly its loop.
 """
 import torch
+
+
+def _active(dist, group=None):
+    return dist is not None and dist.is_initialized() and dist.get_world_size(group) > 1
 
 
 class GradBucket:
@@ -34,10 +47,78 @@ class GradBucket:
     def zero(self):
         self.flat.zero_()
 
-    def all_reduce(self, dist, group=None):
-        """Sum the gradients of all ranks (in place)."""
-        if dist is not None and dist.is_initialized() and dist.get_world_size(group) > 1:
-            dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
+    def all_reduce(self, dist, group=None, async_op=False):
+        """Sum the gradients of all ranks (in place).  async_op: returns the
+        collective's work handle (None when there is nothing to exchange)."""
+        if _active(dist, group):
+            return dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
+        return None
+
+
+class GradExchange:
+    """The per-step gradient exchange of object-sharded data parallelism:
+    model bucket all-reduce (async) + touched code-row all_gather."""
+
+    def __init__(self, model_params, code_tables, dist=None, group=None):
+        self.bucket = GradBucket(model_params)
+        self.tables = list(code_tables)
+        for t in self.tables:
+            t.grad = torch.zeros_like(t)
+        self.dist, self.group = dist, group
+
+    @property
+    def active(self):
+        return _active(self.dist, self.group)
+
+    def zero(self):
+        self.bucket.zero()
+        for t in self.tables:
+            t.grad.zero_()
+
+    def start_model(self):
+        """Launch the model-gradient all-reduce; returns a handle for finish()."""
+        return self.bucket.all_reduce(self.dist, self.group, async_op=True)
+
+    @staticmethod
+    def finish(handle):
+        if handle is not None:
+            handle.wait()
+
+    def exchange_rows(self, rows):
+        """All-gather the gradient rows ``rows`` (object indices this rank
+        rendered, the same count on every rank) of every code table and
+        rebuild the dense gradient tables from them, identically on every
+        rank.  Payload per object: 1 + 256 x n_tables floats."""
+        if not self.active:
+            return
+        dist, group = self.dist, self.group
+        world = dist.get_world_size(group)
+        t0 = self.tables[0]
+        dev = torch.device("cpu") if dist.get_backend(group) == "gloo" else t0.device
+        idx = torch.as_tensor(list(rows), dtype=torch.long, device=t0.device)
+        k = idx.numel()
+        width = sum(t.shape[1] for t in self.tables)
+        mine = torch.empty(k, 1 + width, dtype=torch.float32, device=t0.device)
+        mine[:, 0] = idx.to(torch.float32)              # exact: object counts are far below 2^24
+        off = 1
+        for t in self.tables:
+            mine[:, off:off + t.shape[1]] = t.grad[idx]
+            off += t.shape[1]
+        mine = mine.to(dev)
+        got = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(got, mine, group=group)
+        allrows = torch.cat(got).to(t0.device)          # rank order: identical on every rank
+        rid = allrows[:, 0].long()
+        off = 1
+        for t in self.tables:
+            t.grad.zero_()
+            t.grad.index_add_(0, rid, allrows[:, off:off + t.shape[1]])
+            off += t.shape[1]
+
+    def bytes_per_step(self, rows_per_rank=1):
+        """Bytes each rank contributes to the exchange (fp32)."""
+        width = sum(t.shape[1] for t in self.tables)
+        return {"model_all_reduce": self.bucket.flat.numel() * 4, "code_rows_all_gather": rows_per_rank * (1 + width) * 4}
 
 
 def object_for(step, rank, world, n_objects):
@@ -49,6 +130,6 @@ def object_for(step, rank, world, n_objects):
 
 def broadcast_from(tensors, dist, src=0):
     """Make every rank start from rank ``src``'s values (weights, codes)."""
-    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+    if _active(dist):
         for t in tensors:
             dist.broadcast(t.data, src)

@@ -6,6 +6,7 @@ device pointer tables, and hands torch tensors to the ``cn_*`` entry points
 on torch's current stream.  All arithmetic happens in the HIP library.
 """
 import ctypes
+import os
 
 import torch
 from torch.autograd.graph import increment_version
@@ -14,6 +15,11 @@ from . import _lib
 from ._lib import check, ptr
 
 PRECISIONS = {"fp32": _lib.CN_FP32, "bf16": _lib.CN_BF16}
+# Training-workspace budget per call (bytes): larger images are rendered in
+# ray parts that fit it (render.ImageStep, model.CodeNeRF.forward).  At the
+# srncar net one training sample holds ~8.2 KB (bf16) / ~16 KB (fp32) of
+# activation planes, so 48 GiB is ~6.2 M / ~3.1 M samples per part.
+ACT_BUDGET = int(os.environ.get("CODENERF_ACT_BUDGET", str(48 << 30)))
 
 
 class Engine:
@@ -59,6 +65,16 @@ class Engine:
 
     def dw_ws_bytes(self, M):
         return self.L.cn_dw_ws_bytes(self._plan, M)
+
+    def act_bytes_per_sample(self):
+        return self.L.cn_act_bytes_per_sample(self._plan)
+
+    def max_act_samples(self, budget=None):
+        """Most training samples one workspace of ``budget`` bytes holds
+        (a multiple of the 256-sample tile, at most CN_MAX_SAMPLES)."""
+        b = ACT_BUDGET if budget is None else int(budget)
+        n = (b // self.act_bytes_per_sample()) // 256 * 256
+        return max(256, min(n, self.L.cn_max_samples() // 256 * 256))
 
     def table(self, tensors):
         """Device array of the tensors' data pointers (cached)."""
@@ -117,33 +133,32 @@ class Engine:
     def new_act(self, M):
         return torch.empty(self.act_bytes(M), dtype=torch.uint8, device=self.device)
 
-    def mlp_bwd(self, blob, M, dsigma, drgb, act, codes=False):
-        fn = self.L.cn_mlp_bwd_codes if codes else self.L.cn_mlp_bwd
-        check(fn(self._plan, ptr(self.pack_bwd), ptr(blob), M, ptr(dsigma), ptr(drgb), ptr(act), self.stream),
-              "cn_mlp_bwd")
+    def mlp_bwd(self, blob, M, dsigma, drgb, act, codes=False, act_M=0, row0=0):
+        """dX chain over rows [row0, row0 + pad(M)) of an act_M-sample workspace
+        (act_M 0: M); dsigma / drgb hold the range's rows.  codes: the
+        codes-only variant (stores only the planes mlp_dbias reads)."""
+        fn = self.L.cn_mlp_bwd_codes if codes else self.L.cn_mlp_bwd_rows
+        check(fn(self._plan, ptr(self.pack_bwd), ptr(blob), M, ptr(dsigma), ptr(drgb), ptr(act), int(act_M),
+                 int(row0), self.stream), "cn_mlp_bwd")
 
-    def mlp_bwd_rows(self, blob, M, dsigma, drgb, act, act_M, row0):
-        """dX chain over rows [row0, row0 + pad(M)) of an act_M-sample
-        workspace; dsigma / drgb hold the range's rows."""
-        check(self.L.cn_mlp_bwd_rows(self._plan, ptr(self.pack_bwd), ptr(blob), M, ptr(dsigma), ptr(drgb), ptr(act),
-                                     act_M, row0, self.stream), "cn_mlp_bwd_rows")
-
-    def mlp_dw_rows(self, act, act_M, row0, M, zvec, grads, dbuf, ws, db_accum=False):
-        """Weight gradients over rows [row0, row0 + pad(M)) (grads and, with
-        db_accum, dbuf accumulate)."""
-        check(self.L.cn_mlp_dw_rows(self._plan, ptr(act), act_M, row0, M, ptr(zvec), ptr(self.table(grads)),
-                                    ptr(dbuf), int(bool(db_accum)), ptr(ws), self.stream), "cn_mlp_dw_rows")
-
-    def mlp_dw(self, act, M, zvec, grads, dbuf, ws=None):
+    def mlp_dw(self, act, M, zvec, grads, dbuf, ws=None, act_M=0, row0=0, db_accum=False, nwg=0):
+        """Weight gradients over rows [row0, row0 + pad(M)) (grads accumulate;
+        dbuf is overwritten, or accumulated with db_accum).  ``grads``: the
+        list of gradient tensors or a pointer table from ``table()``;
+        nwg: persistent workgroups (0 = one per CU)."""
         if ws is None:
             ws = torch.empty(self.dw_ws_bytes(M), dtype=torch.uint8, device=self.device)
-        check(self.L.cn_mlp_dw(self._plan, ptr(act), M, ptr(zvec), ptr(self.table(grads)), ptr(dbuf), ptr(ws),
-                               self.stream), "cn_mlp_dw")
+        tab = grads if isinstance(grads, torch.Tensor) else self.table(grads)
+        # the table may be used on a stream other than the one it was made on
+        tab.record_stream(torch.cuda.current_stream(self.device))
+        check(self.L.cn_mlp_dw_rows(self._plan, ptr(act), int(act_M), int(row0), M, ptr(zvec), ptr(tab), ptr(dbuf),
+                                    int(bool(db_accum)), int(nwg), ptr(ws), self.stream), "cn_mlp_dw_rows")
 
-    def mlp_dbias(self, act, M, dbuf, ws=None):
+    def mlp_dbias(self, act, M, dbuf, ws=None, act_M=0):
         if ws is None:
             ws = torch.empty(self.dw_ws_bytes(M), dtype=torch.uint8, device=self.device)
-        check(self.L.cn_mlp_dbias(self._plan, ptr(act), M, ptr(dbuf), ptr(ws), self.stream), "cn_mlp_dbias")
+        check(self.L.cn_mlp_dbias(self._plan, ptr(act), int(act_M), M, ptr(dbuf), ptr(ws), self.stream),
+              "cn_mlp_dbias")
 
     def latent_bwd(self, params, grads, shape_code, texture_code, zvec, dbuf, d_shape, d_tex, reg_coef=0.0,
                    reg_out=None):

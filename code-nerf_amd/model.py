@@ -76,6 +76,13 @@ class CodeNeRF(nn.Module):
 
 
 class _CodeNeRFFunction(torch.autograd.Function):
+    """One fused launch for the forward (plus the latent layers); the backward
+    is the dX chain + weight-gradient pass + latent backward.  A call whose
+    training workspace would exceed the activation budget (engine.ACT_BUDGET)
+    keeps no activations: its forward runs in inference parts and its
+    backward recomputes each part's forward before back-propagating it
+    (gradients of the parts accumulate)."""
+
     @staticmethod
     def forward(ctx, eng, xyz, viewdir, shape_code, texture_code, *params):
         if xyz.shape[-1] != 3 or viewdir.shape != xyz.shape:
@@ -95,26 +102,56 @@ class _CodeNeRFFunction(torch.autograd.Function):
         M = x.shape[0]
         eng.ensure_packed(params, bwd=True)
         blob, zvec = eng.latent_fwd(params, s, t)
-        act = eng.new_act(M) if any(ctx.needs_input_grad[3:]) else None
-        sigma, rgb = eng.mlp_fwd(blob, M, xyz=x, viewdir=v, act=act)
+        need_grad = any(ctx.needs_input_grad[3:])
         ctx.eng, ctx.M, ctx.lead = eng, M, lead
         ctx.code_shapes = (shape_code.shape, texture_code.shape)
-        if act is not None:
+        part = eng.max_act_samples()
+        if need_grad and M <= part:
+            act = eng.new_act(M)
+            sigma, rgb = eng.mlp_fwd(blob, M, xyz=x, viewdir=v, act=act)
+            ctx.part = 0
             ctx.save_for_backward(s, t, blob, zvec, act, *params)
-        return sigma[:M].reshape(*lead, 1), rgb[:M].reshape(*lead, 3)
+            return sigma[:M].reshape(*lead, 1), rgb[:M].reshape(*lead, 3)
+        # inference launches over parts (no workspace)
+        step = eng.L.cn_max_samples() // 256 * 256
+        sigma = torch.empty(M, dtype=torch.float32, device=dev)
+        rgb = torch.empty(M, 3, dtype=torch.float32, device=dev)
+        for a in range(0, M, step):
+            b = min(a + step, M)
+            sg, rg = eng.mlp_fwd(blob, b - a, xyz=x[a:b], viewdir=v[a:b])
+            sigma[a:b] = sg[:b - a]
+            rgb[a:b] = rg[:b - a]
+        if need_grad:
+            ctx.part = part
+            ctx.save_for_backward(s, t, blob, zvec, x, v, *params)
+        return sigma.reshape(*lead, 1), rgb.reshape(*lead, 3)
 
     @staticmethod
     def backward(ctx, g_sigma, g_rgb):
         eng, M = ctx.eng, ctx.M
-        s, t, blob, zvec, act, *params = ctx.saved_tensors
         dsig = (torch.zeros(M, device=eng.device) if g_sigma is None
                 else g_sigma.contiguous().reshape(-1).to(torch.float32))
         drgb = (torch.zeros(M, 3, device=eng.device) if g_rgb is None
                 else g_rgb.contiguous().reshape(-1, 3).to(torch.float32))
-        eng.mlp_bwd(blob, M, dsig, drgb, act)
-        grads = [torch.zeros_like(p) for p in params]
         dbuf = torch.empty(eng.n_inject, 256, dtype=torch.float32, device=eng.device)
-        eng.mlp_dw(act, M, zvec, grads, dbuf)
+        if ctx.part == 0:
+            s, t, blob, zvec, act, *params = ctx.saved_tensors
+            grads = [torch.zeros_like(p) for p in params]
+            eng.mlp_bwd(blob, M, dsig, drgb, act)
+            eng.mlp_dw(act, M, zvec, grads, dbuf)
+        else:
+            # recompute each part's forward into one part-sized workspace
+            s, t, blob, zvec, x, v, *params = ctx.saved_tensors
+            grads = [torch.zeros_like(p) for p in params]
+            gtab = eng.table(grads)
+            P = ctx.part
+            act = eng.new_act(P)
+            ws = torch.empty(eng.dw_ws_bytes(P), dtype=torch.uint8, device=eng.device)
+            for k, a in enumerate(range(0, M, P)):
+                b = min(a + P, M)
+                eng.mlp_fwd(blob, b - a, xyz=x[a:b], viewdir=v[a:b], act=act, act_M=P)
+                eng.mlp_bwd(blob, b - a, dsig[a:b], drgb[a:b], act, act_M=P)
+                eng.mlp_dw(act, b - a, zvec, gtab, dbuf, ws, act_M=P, db_accum=k > 0)
         ds = torch.zeros(256, dtype=torch.float32, device=eng.device)
         dt = torch.zeros(256, dtype=torch.float32, device=eng.device)
         eng.latent_bwd(params, grads, s, t, zvec, dbuf, ds, dt)

@@ -31,10 +31,14 @@ class FusedAdamW:
                         p.grad.zero_()
 
     @torch.no_grad()
-    def step(self):
+    def step(self, groups=None):
+        """groups: indices of the param groups to update (default all) -- a
+        step split over two calls (codes while the model gradients are still
+        being all-reduced, then the model) is the same update as one call."""
         # one launch per (betas, eps, weight_decay) combination; lr is per tensor
         buckets = {}
-        for g in self.param_groups:
+        sel = self.param_groups if groups is None else [self.param_groups[i] for i in groups]
+        for g in sel:
             key = (tuple(g["betas"]), g["eps"], g["weight_decay"])
             for p in g["params"]:
                 if p.grad is None:

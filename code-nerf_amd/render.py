@@ -4,11 +4,20 @@
 (src/trainer.py:65-84, and its twin src/optimizer.py:75-94): rays -> samples
 -> CodeNeRF -> compositing -> chunk-mean MSE (+ code regulariser on chunk 0)
 -> backward into ``.grad`` of the model parameters and the code rows.  The
-reference processes 2048-ray chunks with a host sync per chunk; here the whole
-image is one pass of five launches, with the chunk semantics of the loss
-(gradient = sum of chunk-mean gradients, regulariser counted once) kept
-exactly.  Samples are generated inside the MLP kernel from (ray, z); xyz is
-never materialised.
+reference processes 2048-ray chunks with a host sync per chunk; here an image
+is rendered in as few launches as the activation budget allows, with the
+chunk semantics of the loss (gradient = sum of chunk-mean gradients,
+regulariser counted once) kept exactly.  Samples are generated inside the MLP
+kernel from (ray, z); xyz is never materialised.
+
+Large images (C5: 256^2 rays x 256 samples in fp32) are split into ray parts
+of whole loss chunks whose training workspace fits ``engine.ACT_BUDGET``;
+their gradients accumulate before the caller's optimiser step.
+
+Backward schedule: the rows of a part (coarse rows, then fine rows) are cut
+into ``bwd_ranges`` row ranges; the dX chain of range i runs on the current
+stream while the weight-gradient pass of range i-1 runs on a side stream
+(the dX chain is MFMA-bound, dW streams its operand planes from HBM).
 """
 import torch
 
@@ -16,28 +25,64 @@ from . import engine as _eng
 
 
 class ImageStep:
-    def __init__(self, model, chunk=2048, reg_coef=1e-4, white_bg=True, timers=None, overlap_dw=True):
+    def __init__(self, model, chunk=2048, reg_coef=1e-4, white_bg=True, timers=None, overlap_dw=True,
+                 bwd_ranges=2, dw_side_wgs=0, act_budget=None, max_rays=None):
         self.model = model
-        # coarse + fine step: weight gradients of the fine rows on a second
-        # stream while the dX chain runs over the coarse rows
-        self.overlap_dw = bool(overlap_dw)
-        self._side = None
         self.timers = timers
         self.chunk = int(chunk)
         self.reg_coef = float(reg_coef)
         self.white_bg = bool(white_bg)
-        self._ws = {}
+        # dX / dW pipelining (see module docstring); overlap_dw False: one dX
+        # launch then one dW launch per part, on the current stream
+        self.overlap_dw = bool(overlap_dw)
+        self.bwd_ranges = max(1, int(bwd_ranges))
+        self.dw_side_wgs = int(dw_side_wgs)      # workgroups of the overlapped dW launches (0: one per CU)
+        self.act_budget = act_budget
+        self.max_rays = max_rays                 # explicit cap on rays per part (tests)
+        self._ws = {}                            # device -> grow-only workspace
+        self._side = {}                          # device -> side stream
 
-    def _buffers(self, eng, M):
-        b = self._ws.get(M)
-        if b is None:
-            if len(self._ws) > 4:
-                self._ws.clear()
-            b = dict(act=eng.new_act(M),
-                     dw=torch.empty(eng.dw_ws_bytes(M), dtype=torch.uint8, device=eng.device),
-                     dbuf=torch.empty(eng.n_inject, 256, dtype=torch.float32, device=eng.device))
-            self._ws[M] = b
-        return b
+    # ------------------------------------------------------------ resources
+    def _workspace(self, eng, M):
+        """Activation workspace for at least M samples (grow-only, per device:
+        every call passes its capacity as act_M, so one workspace serves every
+        part size)."""
+        ws = self._ws.get(eng.device)
+        if ws is None or ws["cap"] < M:
+            cap = eng.pad(M)
+            if ws is not None:
+                self._ws.pop(eng.device)
+                del ws
+            dev = eng.device
+            ws = dict(cap=cap, act=eng.new_act(cap),
+                      dw=torch.empty(eng.dw_ws_bytes(cap), dtype=torch.uint8, device=dev),
+                      dbuf=torch.empty(eng.n_inject, 256, dtype=torch.float32, device=dev),
+                      sig=torch.empty(cap, dtype=torch.float32, device=dev),
+                      rgb=torch.empty(cap, 3, dtype=torch.float32, device=dev),
+                      dsig=torch.empty(cap, dtype=torch.float32, device=dev),
+                      drgb=torch.empty(cap, 3, dtype=torch.float32, device=dev))
+            self._ws[eng.device] = ws
+        return ws
+
+    def side_stream(self, device):
+        s = self._side.get(device)
+        if s is None:
+            s = torch.cuda.Stream(device)
+            self._side[device] = s
+        return s
+
+    def ray_parts(self, eng, R, n_per_ray):
+        """Contiguous ray ranges [(a, b)] of whole loss chunks whose training
+        workspace (pad(rays x coarse) + rays x fine samples) fits the budget."""
+        cap = eng.max_act_samples(self.act_budget)
+        per = (cap - 256) // n_per_ray
+        if self.max_rays:
+            per = min(per, int(self.max_rays))
+        per = per // self.chunk * self.chunk
+        if per <= 0:
+            raise ValueError(f"a loss chunk of {self.chunk} rays x {n_per_ray} samples does not fit the "
+                             f"activation budget ({cap} samples): lower the chunk or raise CODENERF_ACT_BUDGET")
+        return [(a, min(a + per, R)) for a in range(0, R, per)]
 
     @staticmethod
     def ensure_grads(tensors):
@@ -46,62 +91,148 @@ class ImageStep:
                 p.grad = torch.zeros_like(p)
         return [p.grad for p in tensors]
 
+    # ------------------------------------------------------------ backward
+    def _bwd_dw(self, eng, blob, ws, zvec, gtab, M):
+        """dX chain + weight gradients over rows [0, M) of the workspace
+        (dsig / drgb rows already hold the upstream gradients, padding rows 0),
+        pipelined over row ranges on two streams when overlap_dw is set."""
+        tm = self.timers
+        cap, act = ws["cap"], ws["act"]
+        dsig, drgb = ws["dsig"], ws["drgb"]
+        Mp = eng.pad(M)
+        k = self.bwd_ranges if self.overlap_dw else 1
+        k = max(1, min(k, Mp // 256))
+        cuts = [(Mp // 256) * i // k * 256 for i in range(k)] + [M]
+        ranges = [(cuts[i], cuts[i + 1] - cuts[i]) for i in range(k)]
+
+        def bwd(r0, n):
+            ev = tm.mark("bwd") if tm else None
+            eng.mlp_bwd(blob, n, dsig[r0:], drgb[r0:], act, act_M=cap, row0=r0)
+            if tm:
+                tm.done("bwd", ev)
+
+        def dw(r0, n, i, nwg):
+            ev = tm.mark("dw") if tm else None
+            eng.mlp_dw(act, n, zvec, gtab, ws["dbuf"], ws["dw"], act_M=cap, row0=r0, db_accum=i > 0, nwg=nwg)
+            if tm:
+                tm.done("dw", ev)
+
+        if k == 1:
+            bwd(0, M)
+            dw(0, M, 0, 0)
+            return
+        main = torch.cuda.current_stream(eng.device)
+        side = self.side_stream(eng.device)
+        bwd(*ranges[0])
+        for i in range(1, k + 1):
+            ready = torch.cuda.Event()
+            ready.record(main)
+            side.wait_event(ready)
+            with torch.cuda.stream(side):
+                # the last range's dW runs alone: every CU
+                dw(*ranges[i - 1], i - 1, self.dw_side_wgs if i < k else 0)
+            if i < k:
+                bwd(*ranges[i])
+        main.wait_stream(side)
+
+    # ------------------------------------------------------------ steps
     def forward_backward(self, rays_o, viewdirs, z_vals, gt, shape_table, texture_table, obj_idx,
                          reg=True, weight_grads=True):
         """One image: returns (chunk losses [ceil(R/chunk)], rendered rgb [R,3],
         reg loss [1]).  Gradients are accumulated into .grad.  weight_grads
         False (codes-only optimisation, src/optimizer.py): the weight-gradient
         pass is replaced by the bias sums the code gradients need."""
-        model = self.model
-        eng = model.engine()
-        params = model.param_list()
+        eng = self.model.engine()
+        R = rays_o.shape[0]
+        N = z_vals.shape[-1]
+        z = z_vals.contiguous().to(eng.device, torch.float32)
+        losses, rgbs, regs = [], [], []
+        for k, (a, b) in enumerate(self.ray_parts(eng, R, N)):
+            zp = z if z.dim() == 1 else z[a:b]
+            l, c, r = self._coarse_part(eng, rays_o[a:b], viewdirs[a:b], zp, gt[a:b], shape_table, texture_table,
+                                        obj_idx, reg and k == 0, weight_grads)
+            losses.append(l)
+            rgbs.append(c)
+            regs.append(r)
+        if len(losses) == 1:
+            return losses[0], rgbs[0], regs[0]
+        return torch.cat(losses), torch.cat(rgbs), regs[0]
+
+    def _coarse_part(self, eng, rays_o, viewdirs, z, gt, shape_table, texture_table, obj_idx, reg, weight_grads):
+        params = self.model.param_list()
         grads = self.ensure_grads(params)
         self.ensure_grads([shape_table, texture_table])
         R = rays_o.shape[0]
-        N = z_vals.shape[-1]
+        N = z.shape[-1]
         M = R * N
-        z = z_vals.contiguous().to(eng.device, torch.float32)
         z_stride = 0 if z.dim() == 1 else N
-        buf = self._buffers(eng, M)
+        ws = self._workspace(eng, M)
+        cap = ws["cap"]
+        Mp = eng.pad(M)
         eng.ensure_packed(params, bwd=True)
         s, t = shape_table.detach()[obj_idx], texture_table.detach()[obj_idx]
         blob, zvec = eng.latent_fwd(params, s, t)
         tm = self.timers
         ev = tm.mark("fwd") if tm else None
-        sigma, rgb = eng.mlp_fwd(blob, M, rays_o=rays_o, rays_d=viewdirs, z=z, z_stride=z_stride,
-                                 n_samples=N, act=buf["act"], codes=not weight_grads)
+        sigma, rgb = eng.mlp_fwd(blob, M, rays_o=rays_o, rays_d=viewdirs, z=z, z_stride=z_stride, n_samples=N,
+                                 act=ws["act"], act_M=cap, act_row0=0, sigma=ws["sig"][:Mp], rgb=ws["rgb"][:Mp],
+                                 codes=not weight_grads)
         if tm:
             tm.done("fwd", ev)
-        out_rgb, chunk_loss, dsig, drgb = _eng.render_loss(sigma, rgb, z, R, N, gt, self.chunk, self.white_bg)
-        ev = tm.mark("bwd") if tm else None
-        eng.mlp_bwd(blob, M, dsig, drgb, buf["act"], codes=not weight_grads)
-        if tm:
-            tm.done("bwd", ev)
-            ev = tm.mark("dw")
+        dsig, drgb = ws["dsig"], ws["drgb"]
+        dsig[M:Mp].zero_()
+        drgb[M:Mp].zero_()
+        out_rgb, chunk_loss, _, _ = _eng.render_loss(sigma, rgb, z, R, N, gt, self.chunk, self.white_bg,
+                                                     dsig=dsig[:M], drgb=drgb[:M])
         if weight_grads:
-            eng.mlp_dw(buf["act"], M, zvec, grads, buf["dbuf"], buf["dw"])
+            self._bwd_dw(eng, blob, ws, zvec, eng.table(grads), M)
         else:
-            eng.mlp_dbias(buf["act"], M, buf["dbuf"], buf["dw"])
-            grads = buf.setdefault("scratch_grads", [torch.zeros_like(p) for p in params])
-        if tm:
-            tm.done("dw", ev)
+            ev = tm.mark("bwd") if tm else None
+            eng.mlp_bwd(blob, M, dsig, drgb, ws["act"], codes=True, act_M=cap, row0=0)
+            if tm:
+                tm.done("bwd", ev)
+                ev = tm.mark("dw")
+            eng.mlp_dbias(ws["act"], M, ws["dbuf"], ws["dw"], act_M=cap)
+            if tm:
+                tm.done("dw", ev)
+            grads = ws.setdefault("scratch_grads", [torch.zeros_like(p) for p in params])
         reg_out = torch.zeros(1, dtype=torch.float32, device=eng.device)
-        eng.latent_bwd(params, grads, s, t, zvec, buf["dbuf"], shape_table.grad[obj_idx],
+        eng.latent_bwd(params, grads, s, t, zvec, ws["dbuf"], shape_table.grad[obj_idx],
                        texture_table.grad[obj_idx], self.reg_coef if reg else 0.0, reg_out)
         return chunk_loss, out_rgb, reg_out
 
     def forward_backward_fine(self, rays_o, viewdirs, z_c, rand_f, gt, shape_table, texture_table, obj_idx,
-                              reg=True):
+                              reg=True, z_f=None):
         """Coarse + fine image step (the BASELINE configs' "64 + 64"; no
         reference counterpart -- NeRF hierarchical sampling through the one
         CodeNeRF MLP, oracle/ref_cpu.py:fine_image_step).  Loss = coarse
         chunk-mean MSE + fine chunk-mean MSE (+ code regulariser once).  The
         coarse pass fills activation rows [0, pad(R*Nc)), the fine pass the
-        rows after, so one backward and one dW cover both.
+        rows after, so one backward schedule covers both.
+        z_f (R, Nf), optional: fine samples to use instead of sample_pdf's
+        (tests replaying one sampling under two precisions); rand_f is then
+        only read for Nf.
         Returns (coarse chunk losses, fine chunk losses, fine rgb (R,3), reg)."""
-        model = self.model
-        eng = model.engine()
-        params = model.param_list()
+        eng = self.model.engine()
+        R = rays_o.shape[0]
+        Nc, Nf = z_c.shape[-1], rand_f.shape[-1]
+        z_c = z_c.contiguous().to(eng.device, torch.float32)
+        outs, zfs = [], []
+        for k, (a, b) in enumerate(self.ray_parts(eng, R, Nc + Nf)):
+            zp = z_c if z_c.dim() == 1 else z_c[a:b]
+            outs.append(self._fine_part(eng, rays_o[a:b], viewdirs[a:b], zp, rand_f[a:b], gt[a:b], shape_table,
+                                        texture_table, obj_idx, reg and k == 0,
+                                        None if z_f is None else z_f[a:b].contiguous()))
+            zfs.append(self.last_z_f)
+        if len(outs) == 1:
+            return outs[0]
+        self.last_z_f = torch.cat(zfs)
+        return (torch.cat([o[0] for o in outs]), torch.cat([o[1] for o in outs]), torch.cat([o[2] for o in outs]),
+                outs[0][3])
+
+    def _fine_part(self, eng, rays_o, viewdirs, z_c, rand_f, gt, shape_table, texture_table, obj_idx, reg,
+                   z_f=None):
+        params = self.model.param_list()
         grads = self.ensure_grads(params)
         self.ensure_grads([shape_table, texture_table])
         R = rays_o.shape[0]
@@ -111,93 +242,48 @@ class ImageStep:
         Mc_p = eng.pad(Mc)
         M = Mc_p + Mf
         Mp = eng.pad(M)
-        z_c = z_c.contiguous().to(eng.device, torch.float32)
-        buf = self._buffers(eng, M)
-        if "sig" not in buf:
-            buf.update(sig=torch.empty(Mp, dtype=torch.float32, device=eng.device),
-                       rgb=torch.empty(Mp, 3, dtype=torch.float32, device=eng.device),
-                       dsig=torch.empty(Mp, dtype=torch.float32, device=eng.device),
-                       drgb=torch.empty(Mp, 3, dtype=torch.float32, device=eng.device))
-        sig, rgb, dsig, drgb = buf["sig"], buf["rgb"], buf["dsig"], buf["drgb"]
-        dsig.zero_()
-        drgb.zero_()
+        ws = self._workspace(eng, M)
+        cap = ws["cap"]
+        sig, rgb, dsig, drgb = ws["sig"], ws["rgb"], ws["dsig"], ws["drgb"]
+        dsig[:Mp].zero_()
+        drgb[:Mp].zero_()
         eng.ensure_packed(params, bwd=True)
         s, t = shape_table.detach()[obj_idx], texture_table.detach()[obj_idx]
         blob, zvec = eng.latent_fwd(params, s, t)
         tm = self.timers
         ev = tm.mark("fwd") if tm else None
         sig_c, rgb_c = eng.mlp_fwd(blob, Mc, rays_o=rays_o, rays_d=viewdirs, z=z_c,
-                                   z_stride=0 if z_c.dim() == 1 else Nc, n_samples=Nc, act=buf["act"], act_M=M,
+                                   z_stride=0 if z_c.dim() == 1 else Nc, n_samples=Nc, act=ws["act"], act_M=cap,
                                    act_row0=0, sigma=sig[:Mc_p], rgb=rgb[:Mc_p])
         if tm:
             tm.done("fwd", ev)
         _, loss_c, _, _ = _eng.render_loss(sig_c, rgb_c, z_c, R, Nc, gt, self.chunk, self.white_bg,
                                            dsig=dsig[:Mc], drgb=drgb[:Mc])
-        z_f = _eng.sample_pdf(sig_c, z_c, R, Nc, rand_f)
+        if z_f is None:
+            z_f = _eng.sample_pdf(sig_c, z_c, R, Nc, rand_f)
+        else:
+            z_f = z_f.to(eng.device, torch.float32)
         ev = tm.mark("fwd") if tm else None
         sig_f, rgb_f = eng.mlp_fwd(blob, Mf, rays_o=rays_o, rays_d=viewdirs, z=z_f, z_stride=Nf, n_samples=Nf,
-                                   act=buf["act"], act_M=M, act_row0=Mc_p, sigma=sig[Mc_p:], rgb=rgb[Mc_p:])
+                                   act=ws["act"], act_M=cap, act_row0=Mc_p, sigma=sig[Mc_p:Mp],
+                                   rgb=rgb[Mc_p:Mp])
         if tm:
             tm.done("fwd", ev)
         out_f, loss_f = _eng.render_loss_fine(sig_c, rgb_c, z_c, Nc, sig_f, rgb_f, z_f, Nf, R, gt, self.chunk,
                                               dsig[:Mc], drgb[:Mc], dsig[Mc_p:Mc_p + Mf],
                                               drgb[Mc_p:Mc_p + Mf], self.white_bg)
-        if self.overlap_dw:
-            self._bwd_dw_overlapped(eng, blob, buf, dsig, drgb, zvec, grads, Mc, Mc_p, Mf, M)
-        else:
-            ev = tm.mark("bwd") if tm else None
-            eng.mlp_bwd(blob, M, dsig, drgb, buf["act"])
-            if tm:
-                tm.done("bwd", ev)
-                ev = tm.mark("dw")
-            eng.mlp_dw(buf["act"], M, zvec, grads, buf["dbuf"], buf["dw"])
-            if tm:
-                tm.done("dw", ev)
+        self._bwd_dw(eng, blob, ws, zvec, eng.table(grads), M)
         reg_out = torch.zeros(1, dtype=torch.float32, device=eng.device)
-        eng.latent_bwd(params, grads, s, t, zvec, buf["dbuf"], shape_table.grad[obj_idx],
+        eng.latent_bwd(params, grads, s, t, zvec, ws["dbuf"], shape_table.grad[obj_idx],
                        texture_table.grad[obj_idx], self.reg_coef if reg else 0.0, reg_out)
         self.last_z_f = z_f
         return loss_c, loss_f, out_f, reg_out
 
-    def _bwd_dw_overlapped(self, eng, blob, buf, dsig, drgb, zvec, grads, Mc, Mc_p, Mf, M):
-        """dX chain over the fine rows, then (current stream) the dX chain over
-        the coarse rows while (side stream) dW reduces the fine rows, then dW
-        of the coarse rows.  Same rows and sums as one mlp_bwd + mlp_dw over
-        [0, M); the fp32 partial order differs.  dW is HBM-bound (operand
-        stream), the dX chain MFMA-bound, so the two share the chip."""
-        tm = self.timers
-        act = buf["act"]
-        main = torch.cuda.current_stream(eng.device)
-        if self._side is None:
-            self._side = torch.cuda.Stream(eng.device)
-        side = self._side
-        ev = tm.mark("bwd") if tm else None
-        eng.mlp_bwd_rows(blob, Mf, dsig[Mc_p:], drgb[Mc_p:], act, M, Mc_p)
-        fine_done = torch.cuda.Event()
-        fine_done.record(main)
-        side.wait_event(fine_done)
-        eng.mlp_bwd_rows(blob, Mc, dsig, drgb, act, M, 0)
-        if tm:
-            tm.done("bwd", ev)
-        coarse_done = torch.cuda.Event()
-        coarse_done.record(main)
-        with torch.cuda.stream(side):
-            # timers: one span per dW launch, each from the moment its rows are
-            # ready (and the side stream free) to its end
-            ev = tm.mark("dw") if tm else None
-            eng.mlp_dw_rows(act, M, Mc_p, Mf, zvec, grads, buf["dbuf"], buf["dw"], db_accum=False)
-            if tm:
-                tm.done("dw", ev)
-            side.wait_event(coarse_done)
-            ev = tm.mark("dw") if tm else None
-            eng.mlp_dw_rows(act, M, 0, Mc, zvec, grads, buf["dbuf"], buf["dw"], db_accum=True)
-            if tm:
-                tm.done("dw", ev)
-        main.wait_stream(side)
-
+    # ------------------------------------------------------------ inference
     @torch.no_grad()
     def render(self, rays_o, viewdirs, z_vals, shape_code, texture_code):
-        """Forward only (src/optimizer.py:108-124): -> rgb (R,3), depth (R,)."""
+        """Forward only (src/optimizer.py:108-124): -> rgb (R,3), depth (R,).
+        No workspace; images beyond CN_MAX_SAMPLES samples go in ray parts."""
         eng = self.model.engine()
         params = self.model.param_list()
         R = rays_o.shape[0]
@@ -205,6 +291,16 @@ class ImageStep:
         z = z_vals.contiguous().to(eng.device, torch.float32)
         eng.ensure_packed(params, bwd=False)
         blob, _ = eng.latent_fwd(params, shape_code.reshape(-1).contiguous(), texture_code.reshape(-1).contiguous())
-        sigma, rgb = eng.mlp_fwd(blob, R * N, rays_o=rays_o, rays_d=viewdirs, z=z,
-                                 z_stride=0 if z.dim() == 1 else N, n_samples=N)
-        return _eng.composite_fwd(sigma, rgb, z, R, N, self.white_bg)
+        per = max(1, (eng.L.cn_max_samples() - 256) // N)
+        rgbs, depths = [], []
+        for a in range(0, R, per):
+            b = min(a + per, R)
+            zp = z if z.dim() == 1 else z[a:b]
+            sigma, rgb = eng.mlp_fwd(blob, (b - a) * N, rays_o=rays_o[a:b], rays_d=viewdirs[a:b], z=zp,
+                                     z_stride=0 if zp.dim() == 1 else N, n_samples=N)
+            c, d = _eng.composite_fwd(sigma, rgb, zp, b - a, N, self.white_bg)
+            rgbs.append(c)
+            depths.append(d)
+        if len(rgbs) == 1:
+            return rgbs[0], depths[0]
+        return torch.cat(rgbs), torch.cat(depths)

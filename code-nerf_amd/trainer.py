@@ -67,7 +67,8 @@ class Trainer:
         self.niter, self.nepoch = 0, 0
         self.check_iter = int(check_iter)
         self.step_impl = ImageStep(self.model, chunk=self.B, reg_coef=self.hpams["loss_reg_coef"])
-        self.bucket = dp.GradBucket(self.model.param_list() + [self.shape_codes.weight, self.texture_codes.weight])
+        self.exchange = dp.GradExchange(self.model.param_list(), [self.shape_codes.weight, self.texture_codes.weight],
+                                        dist)
         self.n_fine = int(self.hpams.get("N_importance", 0))
         self.psnr_log = []
 
@@ -103,7 +104,7 @@ class Trainer:
             H, W, oi = int(H), int(W), int(obj_idx)
             t1 = time.time()
             for k in range(num_instances_per_obj):
-                self.bucket.zero()                                  # zero_grad inside the image loop
+                self.exchange.zero()                                # zero_grad inside the image loop
                 rays_o, viewdir = get_rays(H, W, focal, poses[0, k])
                 z = self._z_vals(self.hpams["N_samples"])
                 gt = imgs[0, k].to(self.device).contiguous()
@@ -115,8 +116,11 @@ class Trainer:
                 else:
                     loss_per_img, rgb, reg = self.step_impl.forward_backward(
                         rays_o, viewdir, z, gt, self.shape_codes.weight, self.texture_codes.weight, oi)
-            self.bucket.all_reduce(self.dist)
-            self.opts.step()
+            work = self.exchange.start_model()           # data parallel: async model all-reduce
+            self.exchange.exchange_rows([oi])            # + the touched code rows
+            self.opts.step(groups=[1, 2])
+            self.exchange.finish(work)
+            self.opts.step(groups=[0])
             mse = float(loss_per_img.mean())
             self.log_psnr_time(mse, time.time() - t1, oi, float(reg))
             if self.check_iter and self.niter % self.check_iter == 0:

@@ -31,9 +31,16 @@
 extern "C" {
 #endif
 
-#define CN_ABI_VERSION 1
+#define CN_ABI_VERSION 2
 #define CN_FP32 0 /* exact-fp32 MFMA path (parity) */
 #define CN_BF16 1 /* bf16 operands, fp32 accumulate (throughput) */
+/* Largest sample count (M, act_M, R * N) one call accepts: the kernels index
+ * samples with 32-bit integers (3 m, 4 m).  Larger images are rendered in
+ * ray parts (codenerf_amd.render.ImageStep / CodeNeRF.forward split
+ * automatically); a call above the limit returns -1 with cn_last_error().
+ * The activation planes have no 4 GB limit: every wave addresses its own
+ * 32-sample slab through a 64-bit descriptor base. */
+#define CN_MAX_SAMPLES (1 << 28)
 
 typedef struct cn_plan cn_plan;
 
@@ -41,7 +48,9 @@ int cn_abi_version(void);
 const char *cn_last_error(void);
 
 /* ---- plan: static layout for one network configuration and precision.
- * Replaces CodeNeRF.__init__ (src/model.py:11-34).  Supported:
+ * Replaces CodeNeRF.__init__ (src/model.py:11-34).  Creating a plan and the
+ * size queries need no device (tables go up with the first cn_pack_weights).
+ * Supported:
  * W = latent_dim = 256, num_xyz_freq = 10, num_dir_freq = 4,
  * (shape_blocks, texture_blocks) in {(3,1), (2,1)}. */
 int cn_plan_create(int shape_blocks, int texture_blocks, int W, int num_xyz_freq,
@@ -49,7 +58,9 @@ int cn_plan_create(int shape_blocks, int texture_blocks, int W, int num_xyz_freq
 void cn_plan_destroy(cn_plan *plan);
 int cn_plan_num_params(const cn_plan *plan);        /* tensors in the state_dict */
 int cn_plan_num_inject(const cn_plan *plan);        /* shape + texture blocks */
-int cn_pad_samples(const cn_plan *plan, int M);     /* M rounded to the tile */
+int cn_pad_samples(const cn_plan *plan, int M);     /* M rounded to the tile (-1: M invalid) */
+int cn_max_samples(void);                           /* CN_MAX_SAMPLES */
+size_t cn_act_bytes_per_sample(const cn_plan *plan); /* workspace bytes per sample (splitting) */
 size_t cn_packed_bytes(const cn_plan *plan, int bwd); /* packed weights */
 size_t cn_blob_floats(const cn_plan *plan);         /* per-call bias blob */
 size_t cn_act_bytes(const cn_plan *plan, int M);    /* training activations */
@@ -98,7 +109,7 @@ int cn_mlp_bwd_rows(const cn_plan *plan, const void *d_pack_bwd, const float *d_
 
 /* ---- codes-only optimisation (src/optimizer.py:75-98: the model is fixed,
  * only the latent codes are updated).  Same arguments as cn_mlp_fwd /
- * cn_mlp_bwd (d_act required); the forward stores only what the backward
+ * cn_mlp_bwd_rows (d_act required); the forward stores only what the backward
  * needs (ReLU masks, sigma pre-activations), the backward only the gradient
  * planes of the layers fed by a code -- what cn_mlp_dbias reads -- and none of
  * the weight-gradient operands. */
@@ -108,7 +119,8 @@ int cn_mlp_fwd_codes(const cn_plan *plan, const void *d_pack_fwd, const float *d
                      float *d_sigma, float *d_rgb, void *d_act, int act_M, int act_row0,
                      void *stream);
 int cn_mlp_bwd_codes(const cn_plan *plan, const void *d_pack_bwd, const float *d_blob, int M,
-                     const float *d_dsigma, const float *d_drgb, void *d_act, void *stream);
+                     const float *d_dsigma, const float *d_drgb, void *d_act, int act_M,
+                     int act_row0, void *stream);
 
 /* ---- weight / bias gradients, accumulated into d_grads; d_dbuf
  * (num_inject x 256) receives this call's bias gradient of every layer fed by
@@ -119,16 +131,21 @@ int cn_mlp_dw(const cn_plan *plan, void *d_act, int M, const float *d_zvec,
 /* ---- cn_mlp_dw over rows [act_row0, act_row0 + pad(M)) of a workspace laid
  * out for act_M samples (act_row0 a multiple of 256).  db_accum != 0 adds
  * this range's bias gradients into d_dbuf instead of overwriting it (the
- * second range of a step).  Grads accumulate as in cn_mlp_dw. */
+ * later ranges of a step).  Grads accumulate as in cn_mlp_dw.
+ * n_workgroups: persistent workgroups of the pass (0 = one per CU, 256);
+ * fewer leave CUs to a dX chain running beside it on another stream (at
+ * least 26: a workgroup's share must not span more than two layers). */
 int cn_mlp_dw_rows(const cn_plan *plan, void *d_act, int act_M, int act_row0, int M,
                    const float *d_zvec, float *const *d_grads, float *d_dbuf, int db_accum,
-                   void *d_ws, void *stream);
+                   int n_workgroups, void *d_ws, void *stream);
 
 /* ---- bias gradients of the layers after each code injection only (d_dbuf
  * [n_inject][256], as cn_mlp_dw writes them), for codes-only optimisation
  * (src/optimizer.py:92: the model is fixed, only the codes are updated, so
- * no weight gradients are needed).  d_ws: cn_dw_ws_bytes(plan, M) bytes. */
-int cn_mlp_dbias(const cn_plan *plan, void *d_act, int M, float *d_dbuf, void *d_ws, void *stream);
+ * no weight gradients are needed), over rows [0, pad(M)) of a workspace laid
+ * out for act_M samples (act_M <= 0: M).  d_ws: cn_dw_ws_bytes(plan, M) bytes. */
+int cn_mlp_dbias(const cn_plan *plan, void *d_act, int act_M, int M, float *d_dbuf, void *d_ws,
+                 void *stream);
 
 /* ---- latent layers + code gradients (+ the code regulariser of
  * src/trainer.py:76-78 when reg_coef != 0; d_reg_out += reg value).

@@ -28,7 +28,7 @@ def test_library_loads_and_exports_every_symbol():
     lib = L.load_library()
     for name in declared_symbols():
         assert hasattr(lib, name), name
-    assert lib.cn_abi_version() == 1
+    assert lib.cn_abi_version() == L.ABI_VERSION
 
 
 def test_no_cpu_fallback():
@@ -50,3 +50,54 @@ def test_state_dict_names_match_reference():
     m = CodeNeRF(3, 1)
     sd = m.state_dict()
     assert [(k, tuple(v.shape)) for k, v in sd.items()] == [(k, tuple(s)) for k, s in param_specs(3, 1)]
+
+
+def _plan(lib, precision=1):
+    import ctypes
+    h = ctypes.c_void_p()
+    assert lib.cn_plan_create(3, 1, 256, 10, 4, 256, precision, ctypes.byref(h)) == 0, lib.cn_last_error()
+    return h
+
+
+def test_plan_and_size_queries_need_no_device():
+    import codenerf_amd._lib as L
+    if not os.path.exists(L.LIB_PATH):
+        pytest.skip("library not built")
+    lib = L.load_library()
+    for prec in (0, 1):
+        h = _plan(lib, prec)
+        assert lib.cn_plan_num_params(h) == 28
+        assert lib.cn_pad_samples(h, 1) == 256
+        assert lib.cn_pad_samples(h, lib.cn_max_samples() + 1) == -1
+        per = lib.cn_act_bytes_per_sample(h)
+        # bf16: ~8.2 KB of planes per training sample, fp32 about twice that
+        assert (7_000 if prec else 14_000) < per < (9_000 if prec else 18_000)
+        assert lib.cn_act_bytes(h, 1 << 20) == per << 20
+        lib.cn_plan_destroy(h)
+
+
+@pytest.mark.parametrize("fn", ["cn_mlp_fwd", "cn_mlp_bwd", "cn_mlp_dw"])
+def test_sample_guard_rejects_oversized_calls(fn):
+    """A call over CN_MAX_SAMPLES samples fails with -1 and a message before
+    anything is launched (the kernels index samples with 32-bit integers),
+    instead of wrapping silently."""
+    import ctypes
+    import codenerf_amd._lib as L
+    if not os.path.exists(L.LIB_PATH):
+        pytest.skip("library not built")
+    lib = L.load_library()
+    h = _plan(lib)
+    big = lib.cn_max_samples() + 256
+    d = ctypes.c_void_p(16)          # never dereferenced: validation comes first
+    if fn == "cn_mlp_fwd":
+        rc = lib.cn_mlp_fwd(h, d, d, big, None, None, d, d, d, 0, 64, d, d, d, big, 0, None)
+    elif fn == "cn_mlp_bwd":
+        rc = lib.cn_mlp_bwd(h, d, d, big, d, d, d, None)
+    else:
+        rc = lib.cn_mlp_dw(h, d, big, d, d, d, d, None)
+    assert rc == -1
+    assert b"CN_MAX_SAMPLES" in lib.cn_last_error()
+    # a workspace laid out for more rows than the guard allows is refused too
+    rc = lib.cn_mlp_bwd_rows(h, d, d, 256, d, d, d, big, 0, None)
+    assert rc == -1 and b"CN_MAX_SAMPLES" in lib.cn_last_error()
+    lib.cn_plan_destroy(h)

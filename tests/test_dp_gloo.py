@@ -1,7 +1,8 @@
 """Data-parallel semantics on CPU: world_size-2 gloo (the GPU path runs the
 same code over RCCL).  Each rank renders its own object with the oracle's
-image step, the gradient bucket (codenerf_amd.dp.GradBucket) is summed with
-one all-reduce, and every rank applies AdamW.  Checked: replicas identical
+image step; the model gradient bucket is summed by one async all-reduce and
+the touched code-table rows are all-gathered (codenerf_amd.dp.GradExchange);
+every rank applies AdamW.  Checked: replicas identical
 after the step, and equal to one process that accumulates both objects'
 gradients before the same AdamW step (1 GPU with 1 object
 per step is the reference; N ranks sum N objects' gradients)."""
@@ -39,16 +40,18 @@ def _opt(p, st, tt):
 def _worker(rank, world, port, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from codenerf_amd.dp import GradBucket, object_for
+    from codenerf_amd.dp import GradExchange, object_for
     torch.set_num_threads(1)
     p, st, tt, ro, vd, z, gts = _setup()
-    bucket = GradBucket(list(p.values()) + [st, tt])
+    ex = GradExchange(list(p.values()), [st, tt], dist)
     opt = _opt(p, st, tt)
     for step in range(2):
-        bucket.zero()
+        ex.zero()
         obj = object_for(step, rank, world, N_OBJ)
         ref_cpu.image_step(p, st, tt, obj, ro, vd, z, gts[obj], chunk=16)
-        bucket.all_reduce(dist)
+        work = ex.start_model()          # async model all-reduce
+        ex.exchange_rows([obj])          # all_gather of the touched code rows
+        ex.finish(work)
         opt.step()
     flat = torch.cat([t.detach().reshape(-1) for t in list(p.values()) + [st, tt]])
     gathered = [torch.empty_like(flat) for _ in range(world)]
@@ -69,7 +72,7 @@ def _free_port():
 
 @pytest.mark.timeout(300)
 def test_two_rank_step_matches_summed_single_process():
-    from codenerf_amd.dp import GradBucket, object_for
+    from codenerf_amd.dp import GradExchange, object_for
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -84,10 +87,10 @@ def test_two_rank_step_matches_summed_single_process():
     np.testing.assert_array_equal(res[0], res[1])          # replicas bit-identical
     # single process: both ranks' objects accumulated, then the same AdamW step
     p, st, tt, ro, vd, z, gts = _setup()
-    bucket = GradBucket(list(p.values()) + [st, tt])
+    ex = GradExchange(list(p.values()), [st, tt])
     opt = _opt(p, st, tt)
     for step in range(2):
-        bucket.zero()
+        ex.zero()
         for rank in range(world):
             obj = object_for(step, rank, world, N_OBJ)
             ref_cpu.image_step(p, st, tt, obj, ro, vd, z, gts[obj], chunk=16)

@@ -1,0 +1,336 @@
+"""GPU: the BASELINE configurations the bench measures, pinned to the CPU oracle
+at their own precision and size (through the C ABI).
+
+* C2 -- 128^2 rays, 64 coarse + 64 fine samples, bf16, the full train step
+  (forward, compositing + chunk-mean MSE, dX chain, dW, latent backward, AdamW)
+  through ``TrainCore.train_step``:
+    - rendered rgb and the chunk losses of two 2,048-ray chunks against the
+      oracle's fine_image_step (forward, fp32) on the GPU's own fine samples:
+      bf16 tolerance max|d rgb| 3e-2, mean 3e-3, chunk losses rtol 2e-2;
+    - full-image gradients against the HIP fp32 path on the same samples:
+      relative L2 error <= 2e-2 per tensor (measured worst 6.6e-3), cosine
+      >= 0.9995;
+    - the AdamW update against the oracle's AdamWRef on the bf16 gradients.
+* C4 -- optimize.py: 50 views, codes only (src/optimizer.py:73-97), 64^2 x 16:
+  fp32 code gradients against the oracle (rtol 2e-3 of the max), bf16 within
+  relative L2 3e-2 of fp32.
+* C5 -- 256^2, 128 + 128 samples, fp32, one 2,048-ray part against the
+  oracle: rgb / losses rtol 1e-4, gradients rtol 2e-3;
+* the automatic ray-part split (>4 M fp32 samples, the whole C5 image): the
+  first chunk matches the oracle at rtol 1e-4 and the gradients do not depend
+  on where the parts are cut (relative L2 1e-5);
+* the module API over the activation budget (recompute parts) matches the
+  single-workspace backward.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_cpu
+from oracle.params import make_codes, make_params, look_at_pose
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    return torch.device("cuda", 0)
+
+
+def _model(params, precision):
+    from codenerf_amd.model import CodeNeRF
+    m = CodeNeRF(3, 1, precision=precision)
+    m.load_state_dict({k: torch.tensor(v) for k, v in params.items()})
+    return m.to(_dev())
+
+
+def _scene(H, seed, radius=1.3, az=30.0, el=20.0):
+    """c2w (OpenGL) and a ray-cast synthetic target image (R, 3)."""
+    from codenerf_amd.data import _object_spec, _render_object
+    c2w = look_at_pose(radius, az, el)
+    focal = 131.25 * H / 128
+    spec = _object_spec(np.random.Generator(np.random.PCG64(seed)))
+    img = _render_object(spec, c2w.astype(np.float64), H, H, focal)
+    return torch.tensor(c2w), focal, torch.tensor(img.reshape(-1, 3), dtype=torch.float32)
+
+
+def _z(near, far, n, seed):
+    g = torch.Generator().manual_seed(seed)
+    half = (far - near) / (2 * n)
+    return torch.linspace(near + half, far - half, n) + torch.rand(n, generator=g) * (far - near) / (2 * n)
+
+
+def _rel_l2(a, b):
+    a, b = a.double().reshape(-1), b.double().reshape(-1)
+    return float((a - b).norm() / (b.norm() + 1e-30))
+
+
+def _cos(a, b):
+    a, b = a.double().reshape(-1), b.double().reshape(-1)
+    return float(a @ b / (a.norm() * b.norm() + 1e-30))
+
+
+def _fine_fwd(p, st, tt, obj, ro, vd, z_c, z_f, gt):
+    Nc, Nf = z_c.shape[-1], z_f.shape[-1]
+    s, t = st[obj][None], tt[obj][None]
+    xyz = ro[:, None, :] + vd[:, None, :] * z_c[..., None]
+    sig_c, rgb_c = ref_cpu.codenerf_forward(p, xyz, vd[:, None, :].expand(-1, Nc, -1), s, t)
+    rgb, _ = ref_cpu.volume_rendering(sig_c, rgb_c, z_c)
+    lc = float(torch.mean((rgb - gt) ** 2))
+    xyz_f = ro[:, None, :] + vd[:, None, :] * z_f[..., None]
+    sig_f, rgb_f = ref_cpu.codenerf_forward(p, xyz_f, vd[:, None, :].expand(-1, Nf, -1), s, t)
+    z_m, sig_m, rgb_m = ref_cpu.merge_samples(z_c, z_f, (sig_c[..., 0], sig_f[..., 0]), (rgb_c, rgb_f))
+    rgb2, _ = ref_cpu.volume_rendering(sig_m, rgb_m, z_m)
+    lf = float(torch.mean((rgb2 - gt) ** 2))
+    return [lc], [lf], rgb2
+
+
+# ---------------------------------------------------------------- C2
+def test_c2_train_step_bf16_full_image():
+    from codenerf_amd import engine as _eng
+    from codenerf_amd.render import ImageStep
+    from codenerf_amd.trainer_core import TrainCore
+    H, Nc, Nf, n_obj, obj = 128, 64, 64, 4, 1
+    R = H * H
+    params = make_params(21)
+    s0, t0 = make_codes(21, n_obj)
+    c2w, focal, gt = _scene(H, 21)
+    z = _z(0.8, 1.8, Nc, 3)
+    dev = _dev()
+
+    m16 = _model(params, "bf16")
+    st16 = torch.nn.Parameter(torch.tensor(s0, device=dev))
+    tt16 = torch.nn.Parameter(torch.tensor(t0, device=dev))
+    core = TrainCore(m16, st16, tt16, near=0.8, far=1.8, n_coarse=Nc, n_fine=Nf, chunk=2048)
+    core.stratified_z = lambda d: z.to(d)
+    torch.manual_seed(5)
+    (lc, lf), rgb = core.train_step(H, H, focal, c2w.to(dev), gt.to(dev), obj)
+    torch.cuda.synchronize()
+    z_f = core.step_impl.last_z_f.cpu()
+    g16 = {k: p.grad.detach().clone() for k, p in m16.named_parameters()}
+    gs16, gt16 = st16.grad.detach().clone(), tt16.grad.detach().clone()
+    after16 = {k: p.detach().clone() for k, p in m16.named_parameters()}
+    assert lc.numel() == lf.numel() == R // 2048 and rgb.shape == (R, 3)
+
+    # (1) rgb + chunk losses vs the oracle on two chunks, the GPU's own fine samples
+    ro, vd = (t.cpu() for t in _eng.get_rays_dev(H, H, focal, True, c2w.to(dev)))
+    st_c, tt_c = torch.tensor(s0), torch.tensor(t0)
+    p = ref_cpu.param_tensors(params, requires_grad=False)
+    for c in (0, 5):
+        a, b = 2048 * c, 2048 * (c + 1)
+        with torch.no_grad():
+            lcr, lfr, rgbr = _fine_fwd(p, st_c, tt_c, obj, ro[a:b], vd[a:b], z, z_f[a:b], gt[a:b])
+        d = (rgb[a:b].cpu() - rgbr).abs()
+        print(f"C2 chunk {c}: bf16 vs oracle rgb max|d| {float(d.max()):.2e} mean {float(d.mean()):.2e}; "
+              f"loss rel d coarse {abs(float(lc[c]) / lcr[0] - 1):.2e} fine {abs(float(lf[c]) / lfr[0] - 1):.2e}")
+        assert float(d.max()) < 3e-2 and float(d.mean()) < 3e-3, (c, float(d.max()), float(d.mean()))
+        np.testing.assert_allclose(float(lc[c]), lcr[0], rtol=2e-2)
+        np.testing.assert_allclose(float(lf[c]), lfr[0], rtol=2e-2)
+
+    # (2) full-image gradients vs the HIP fp32 path on the same samples
+    m32 = _model(params, "fp32")
+    st32 = torch.nn.Parameter(torch.tensor(s0, device=dev))
+    tt32 = torch.nn.Parameter(torch.tensor(t0, device=dev))
+    step32 = ImageStep(m32, chunk=2048, reg_coef=1e-4)
+    ro_d, vd_d = _eng.get_rays_dev(H, H, focal, True, c2w.to(dev))
+    step32.forward_backward_fine(ro_d, vd_d, z.to(dev), torch.zeros(R, Nf, device=dev), gt.to(dev), st32, tt32, obj,
+                                 z_f=z_f.to(dev))
+    torch.cuda.synchronize()
+    worst = []
+    for k, p32 in m32.named_parameters():
+        e, c = _rel_l2(g16[k], p32.grad), _cos(g16[k], p32.grad)
+        worst.append((e, k, c))
+        assert e <= 2e-2 and c >= 0.9995, (k, e, c)
+    for a16, b32 in ((gs16, st32.grad), (gt16, tt32.grad)):
+        assert _rel_l2(a16[obj], b32[obj]) <= 2e-2, _rel_l2(a16[obj], b32[obj])
+        assert float(a16[torch.arange(n_obj) != obj].abs().max()) == 0.0      # untouched rows
+    print("C2 bf16 vs fp32 gradient rel-L2, worst:", sorted(worst)[-3:])
+
+    # (3) AdamW: the update applied to the bf16 gradients == torch AdamW order
+    ref_p = {k: torch.tensor(v) for k, v in params.items()}
+    for k, v in ref_p.items():
+        v.grad = g16[k].cpu()
+    rs, rt = torch.tensor(s0), torch.tensor(t0)
+    rs.grad, rt.grad = gs16.cpu(), gt16.cpu()
+    ref_cpu.AdamWRef([(list(ref_p.values()), 1e-4), ([rs], 1e-3), ([rt], 1e-3)]).step()
+    for k, v in ref_p.items():
+        np.testing.assert_allclose(after16[k].cpu().numpy(), v.numpy(), rtol=1e-6, atol=1e-9, err_msg=k)
+    np.testing.assert_allclose(st16.detach().cpu().numpy(), rs.numpy(), rtol=1e-6, atol=1e-9)
+
+
+# ---------------------------------------------------------------- C4
+def _c4_views(H, n_views, seed):
+    from codenerf_amd.data import _object_spec, _render_object
+    spec = _object_spec(np.random.Generator(np.random.PCG64(seed)))
+    rng = np.random.Generator(np.random.PCG64(seed + 1))
+    focal = 131.25 * H / 128
+    views = []
+    for _ in range(n_views):
+        c2w = look_at_pose(1.3, rng.uniform(-180, 180), rng.uniform(-5, 50))
+        img = _render_object(spec, c2w.astype(np.float64), H, H, focal)
+        views.append((torch.tensor(c2w), torch.tensor(img.reshape(-1, 3), dtype=torch.float32)))
+    return focal, views
+
+
+def _c4_gpu(precision, params, code0, focal, views, H, N, z):
+    """optimize.py's code step (src/optimizer.py:73-97): zero_grad, every view
+    accumulates into the two code gradients (weights fixed), one AdamW step."""
+    from codenerf_amd import engine as _eng
+    from codenerf_amd.optim import FusedAdamW
+    from codenerf_amd.render import ImageStep
+    dev = _dev()
+    m = _model(params, precision)
+    sc = torch.nn.Parameter(torch.tensor(code0[0], device=dev))
+    tc = torch.nn.Parameter(torch.tensor(code0[1], device=dev))
+    sc.grad, tc.grad = torch.zeros_like(sc), torch.zeros_like(tc)
+    step = ImageStep(m, chunk=2048, reg_coef=1e-4)
+    losses = []
+    for c2w, gt in views:
+        ro, vd = _eng.get_rays_dev(H, H, focal, True, c2w.to(dev))
+        l, _, _ = step.forward_backward(ro, vd, z.to(dev), gt.to(dev), sc, tc, 0, weight_grads=False)
+        losses.append(l)
+    g = (sc.grad.detach().clone(), tc.grad.detach().clone())
+    opt = FusedAdamW([{"params": [sc], "lr": 1e-2}, {"params": [tc], "lr": 1e-2}])
+    opt.step()
+    torch.cuda.synchronize()
+    return g, torch.cat(losses).cpu(), (sc.detach().cpu(), tc.detach().cpu())
+
+
+def test_c4_codes_only_50_views_vs_oracle():
+    H, N, n_views = 64, 16, 50
+    params = make_params(31)
+    s0, t0 = make_codes(31, 1)
+    focal, views = _c4_views(H, n_views, 31)
+    z = _z(0.8, 1.8, N, 4)
+    (gs, gtx), losses, (s1, t1) = _c4_gpu("fp32", params, (s0, t0), focal, views, H, N, z)
+    # oracle: the reference's per-view chunk loop, weights without grad
+    p = ref_cpu.param_tensors(params, requires_grad=False)
+    sc = torch.tensor(s0, requires_grad=True)
+    tc = torch.tensor(t0, requires_grad=True)
+    ref_losses = []
+    for c2w, gt in views:
+        ro, vd = ref_cpu.get_rays(H, H, torch.tensor([focal], dtype=torch.float64), c2w)
+        l, _ = ref_cpu.image_step(p, sc, tc, 0, ro, vd, z, gt, chunk=2048, reg_coef=1e-4)
+        ref_losses += l
+    np.testing.assert_allclose(losses.numpy(), np.array(ref_losses), rtol=1e-4)
+    for a, b in ((gs, sc.grad), (gtx, tc.grad)):
+        a, b = a.cpu().numpy(), b.numpy()
+        np.testing.assert_allclose(a, b, rtol=2e-3, atol=2e-3 * np.abs(b).max())
+    # AdamW on the codes: the GPU update applied to the GPU's gradients == torch's order
+    rs, rt = torch.tensor(s0), torch.tensor(t0)
+    rs.grad, rt.grad = gs.cpu(), gtx.cpu()
+    ref_cpu.AdamWRef([([rs], 1e-2), ([rt], 1e-2)]).step()
+    np.testing.assert_allclose(s1.numpy(), rs.numpy(), rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(t1.numpy(), rt.numpy(), rtol=1e-6, atol=1e-9)
+    # bf16 (the benchmarked precision) against fp32 on the same views
+    (gs16, gt16), l16, _ = _c4_gpu("bf16", params, (s0, t0), focal, views, H, N, z)
+    print(f"C4 bf16 vs fp32 code-gradient rel-L2: shape {_rel_l2(gs16, gs):.2e} texture {_rel_l2(gt16, gtx):.2e}")
+    assert _rel_l2(gs16, gs) <= 3e-2 and _rel_l2(gt16, gtx) <= 3e-2, (_rel_l2(gs16, gs), _rel_l2(gt16, gtx))
+    np.testing.assert_allclose(l16.numpy(), losses.numpy(), rtol=2e-2)
+
+
+# ---------------------------------------------------------------- C5
+def _c5_setup():
+    H, Nc, Nf = 256, 128, 128
+    params = make_params(41)
+    s0, t0 = make_codes(41, 2)
+    c2w, focal, gt = _scene(H, 41)
+    z = _z(0.8, 1.8, Nc, 5)
+    return H, Nc, Nf, params, s0, t0, c2w, focal, gt, z
+
+
+def test_c5_fp32_one_ray_part_vs_oracle():
+    from codenerf_amd import engine as _eng
+    from codenerf_amd.render import ImageStep
+    H, Nc, Nf, params, s0, t0, c2w, focal, gt, z = _c5_setup()
+    dev = _dev()
+    ro, vd = _eng.get_rays_dev(H, H, focal, True, c2w.to(dev))
+    a, b = 20480, 22528                       # one 2,048-ray part through the middle of the image
+    m = _model(params, "fp32")
+    st = torch.nn.Parameter(torch.tensor(s0, device=dev))
+    tt = torch.nn.Parameter(torch.tensor(t0, device=dev))
+    rnd = torch.rand(b - a, Nf, generator=torch.Generator().manual_seed(9))
+    step = ImageStep(m, chunk=2048, reg_coef=1e-4)
+    lc, lf, rgb, _ = step.forward_backward_fine(ro[a:b], vd[a:b], z.to(dev), rnd.to(dev), gt[a:b].to(dev), st, tt, 1)
+    torch.cuda.synchronize()
+    z_f = step.last_z_f.cpu()
+    p = ref_cpu.param_tensors(params)
+    st_r = torch.tensor(s0, requires_grad=True)
+    tt_r = torch.tensor(t0, requires_grad=True)
+    lcr, lfr, rgbr = ref_cpu.fine_image_step(p, st_r, tt_r, 1, ro[a:b].cpu(), vd[a:b].cpu(), z, z_f, gt[a:b],
+                                             chunk=2048)
+    np.testing.assert_allclose(rgb.cpu().numpy(), rgbr.numpy(), rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(lc.cpu().numpy(), np.array(lcr), rtol=1e-4)
+    np.testing.assert_allclose(lf.cpu().numpy(), np.array(lfr), rtol=1e-4)
+    for k, prm in m.named_parameters():
+        x, y = prm.grad.cpu().numpy(), p[k].grad.numpy()
+        np.testing.assert_allclose(x, y, rtol=2e-3, atol=2e-6 * max(1.0, np.abs(y).max()), err_msg=k)
+    for x, y in ((st.grad, st_r.grad), (tt.grad, tt_r.grad)):
+        x, y = x.cpu().numpy(), y.numpy()
+        np.testing.assert_allclose(x, y, rtol=2e-3, atol=2e-6 * max(1.0, np.abs(y).max()))
+
+
+def test_autosplit_fp32_c5_image_above_4m_samples():
+    """The whole C5 image (16.8 M fp32 samples, ~270 GB of activations in one
+    workspace) goes through ImageStep's automatic ray parts."""
+    from codenerf_amd import engine as _eng
+    from codenerf_amd.render import ImageStep
+    H, Nc, Nf, params, s0, t0, c2w, focal, gt, z = _c5_setup()
+    R = H * H
+    dev = _dev()
+    ro, vd = _eng.get_rays_dev(H, H, focal, True, c2w.to(dev))
+    rnd = torch.rand(R, Nf, generator=torch.Generator().manual_seed(11)).to(dev)
+    grads, outs = [], []
+    for max_rays in (None, 4096):
+        m = _model(params, "fp32")
+        st = torch.nn.Parameter(torch.tensor(s0, device=dev))
+        tt = torch.nn.Parameter(torch.tensor(t0, device=dev))
+        step = ImageStep(m, chunk=2048, reg_coef=1e-4, max_rays=max_rays)
+        parts = step.ray_parts(m.engine(), R, Nc + Nf)
+        assert len(parts) > 1 and R * (Nc + Nf) > 4_000_000
+        z_f = None if not outs else outs[0][3].to(dev)
+        lc, lf, rgb, _ = step.forward_backward_fine(ro, vd, z.to(dev), rnd, gt.to(dev), st, tt, 0, z_f=z_f)
+        torch.cuda.synchronize()
+        outs.append((lc.cpu(), lf.cpu(), rgb.cpu(), step.last_z_f.cpu(), len(parts)))
+        grads.append([p.grad.detach().clone() for p in m.parameters()] + [st.grad.clone(), tt.grad.clone()])
+        del m, step
+    assert outs[0][4] != outs[1][4]
+    np.testing.assert_array_equal(outs[0][1].numpy(), outs[1][1].numpy())     # same rays, same arithmetic
+    for a, b in zip(*grads):
+        assert _rel_l2(a, b) <= 1e-5, _rel_l2(a, b)
+    # the first loss chunk against the oracle (forward, fp32)
+    lc, lf, rgb, z_f, _ = outs[0]
+    p = ref_cpu.param_tensors(params, requires_grad=False)
+    with torch.no_grad():
+        lcr, lfr, rgbr = _fine_fwd(p, torch.tensor(s0), torch.tensor(t0), 0, ro[:2048].cpu(), vd[:2048].cpu(), z,
+                                   z_f[:2048], gt[:2048])
+    np.testing.assert_allclose(rgb[:2048].numpy(), rgbr.numpy(), rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(float(lc[0]), lcr[0], rtol=1e-4)
+    np.testing.assert_allclose(float(lf[0]), lfr[0], rtol=1e-4)
+
+
+def test_module_forward_over_budget_recomputes_parts(monkeypatch):
+    """CodeNeRF.forward above the activation budget keeps no workspace and
+    recomputes each part in the backward: same gradients as one workspace."""
+    from codenerf_amd import engine as _eng
+    dev = _dev()
+    params = make_params(51)
+    g = torch.Generator().manual_seed(3)
+    B, N = 1024, 64
+    xyz = (torch.rand(B, N, 3, generator=g) * 2 - 1).to(dev)
+    vdir = torch.nn.functional.normalize(torch.randn(B, N, 3, generator=g), dim=-1).to(dev)
+    out = []
+    for budget in (None, 20_000 * 16 * 1024):
+        if budget:
+            monkeypatch.setattr(_eng, "ACT_BUDGET", budget)
+        m = _model(params, "fp32")
+        assert (m.engine().max_act_samples() < B * N) == bool(budget)
+        s = torch.tensor(make_codes(51, 1)[0], device=dev, requires_grad=True)
+        t = torch.tensor(make_codes(51, 1)[1], device=dev, requires_grad=True)
+        sig, rgb = m(xyz, vdir, s, t)
+        (sig.square().mean() + (rgb * torch.linspace(-1, 1, 3, device=dev)).sum() / B).backward()
+        out.append((sig.detach(), rgb.detach(), [p.grad for p in m.parameters()], s.grad, t.grad))
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    for a, b in zip(out[0][2] + [out[0][3], out[0][4]], out[1][2] + [out[1][3], out[1][4]]):
+        assert _rel_l2(a, b) <= 1e-5

@@ -30,23 +30,28 @@ def _hpams(root, N=16, prec="fp32", n_train_views=4, n_test_views=3):
             "check_points": 1000, "N_importance": 0, "precision": prec}
 
 
-def _oracle_training(hp, init, iters_all, B, n_inst=1):
-    """CPU replay of src/trainer.py:32-102 with the oracle's image step."""
+def _oracle_training(hp, init, iters_all, B, n_inst=1, iters_crop=0):
+    """CPU replay of src/trainer.py:34-96 with the oracle's image step: crop
+    phase (central 64x64 of a 128^2 view, focal unchanged, src/data.py:76-78) while niter < iters_crop, AdamW re-created
+    per epoch, zero_grad inside the per-image loop (only the last of the
+    n_inst images drives the step, src/trainer.py:61-64)."""
     from codenerf_amd.data import SRN, collate_one
     from oracle import ref_cpu
     p = {k: v.clone().requires_grad_() for k, v in init["model"].items()}
     st = init["shape"].clone().requires_grad_()
     tt = init["texture"].clone().requires_grad_()
     d = hp["data"]
-    psnrs, niter = [], 0
+    psnrs, niter, shapes = [], 0, []
     while niter < iters_all:
-        ds = SRN(d["cat"], d["splits"], d["data_dir"], n_inst, crop_img=False, n_train_views=d["n_train_views"])
+        crop = niter < iters_crop
+        limit = iters_crop if crop else iters_all
+        ds = SRN(d["cat"], d["splits"], d["data_dir"], n_inst, crop_img=crop, n_train_views=d["n_train_views"])
         ms, ls = hp["lr_schedule"]
         lr1 = ms["lr"] * 2 ** (-(niter // ms["interval"]))
         lr2 = ls["lr"] * 2 ** (-(niter // ls["interval"]))
         opt = ref_cpu.AdamWRef([(list(p.values()), lr1), ([st], lr2), ([tt], lr2)])
         for idx in range(len(ds)):
-            if niter >= iters_all:
+            if niter >= limit:
                 break
             focal, H, W, imgs, poses, inst, oi = collate_one(ds[idx])
             for k in range(n_inst):
@@ -58,7 +63,9 @@ def _oracle_training(hp, init, iters_all, B, n_inst=1):
                                                reg_coef=hp["loss_reg_coef"])
             opt.step()
             psnrs.append(-10 * np.log(np.mean(losses)) / np.log(10))
+            shapes.append(int(H))
             niter += 1
+    _oracle_training.shapes = shapes
     return psnrs, p, st, tt
 
 
@@ -96,6 +103,38 @@ def test_train_psnr_matches_cpu_replay(tmp_path):
     ck = torch.load(os.path.join(str(tmp_path / "exps"), "t", "models.pth"), map_location="cpu", weights_only=True)
     assert set(ck) == {"model_params", "shape_code_params", "texture_code_params", "niter", "nepoch"}
     assert "weight" in ck["shape_code_params"]
+
+
+def test_crop_phase_and_two_instances_match_cpu_replay(tmp_path):
+    """The reference defaults the other trainer tests leave out: the crop
+    phase (iters_crop > 0: central crop, H and W halved, focal unchanged;
+    src/data.py:76-78, src/trainer.py:39-41) and num_instances_per_obj = 2
+    (train.py:19), where zero_grad inside the image loop leaves only the last
+    image's gradients for the step (src/trainer.py:61-64).  fp32, 0.01 dB."""
+    from codenerf_amd.data import make_synthetic_srn
+    from codenerf_amd.trainer import Trainer
+    root = str(tmp_path / "data")
+    make_synthetic_srn(root, "srn_cars", "cars_train", n_obj=2, n_views=4, H=128, W=128, focal=131.25, seed=8)
+    hp = _hpams(root, N=16)
+    tr = Trainer("t", 0, hpams=hp, batch_size=2048, check_iter=0, exp_root=str(tmp_path / "exps"))
+    init = {"model": {k: v.detach().cpu().clone() for k, v in tr.model.state_dict().items()},
+            "shape": tr.shape_codes.weight.detach().cpu().clone(),
+            "texture": tr.texture_codes.weight.detach().cpu().clone()}
+    iters_crop, iters = 3, 6
+    torch.manual_seed(31)
+    np.random.seed(31)
+    tr.training(iters_crop, iters, 2)
+    torch.manual_seed(31)
+    np.random.seed(31)
+    ref_psnr, p, st, tt = _oracle_training(hp, init, iters, 2048, n_inst=2, iters_crop=iters_crop)
+    # the crop phase really ran on the central 64x64 of the 128x128 views
+    assert _oracle_training.shapes == [64] * 3 + [128] * 3
+    assert len(tr.psnr_log) == len(ref_psnr) == iters
+    np.testing.assert_allclose(np.array(tr.psnr_log), np.array(ref_psnr), atol=0.01)
+    sd = tr.model.state_dict()
+    for k, v in p.items():
+        d = np.abs(sd[k].cpu().numpy() - v.detach().numpy())
+        assert d.max() <= 2 * 6e-4 and np.mean(d <= 1e-6 + 1e-3 * np.abs(v.detach().numpy())) > 0.99, k
 
 
 def test_bf16_train_psnr_within_005db_of_fp32_replay(tmp_path):
