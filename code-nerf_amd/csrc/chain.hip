@@ -74,6 +74,26 @@ CN_DEV uint32_t relu_mask_bf16x2(uint32_t p, uint32_t word) {
       : "=&v"(m2), "=&v"(tmp) : "v"(word), "I"(PA), "I"(PB), "s"(0xFFFFu));
   return p & ~m2;
 }
+// sin and cos of v (radians) on the transcendental unit, for the bf16 path's
+// positional encoding: v / 2 pi in turns with a two-term constant (the
+// product's rounding error recovered by FMA), whole turns removed exactly by
+// v_fract_f32, then v_sin_f32 / v_cos_f32 (input in turns).  Absolute error
+// ~1e-6 at the largest argument (2^9 |x| ~ 1e3 rad), against the 2^-9
+// relative rounding the bf16 operand applies next; the fp32 parity path keeps
+// the correctly rounded sincosf.
+CN_DEV void sincos_turns(float v, float& s, float& c) {
+  constexpr float kHi = 0.15915493667125702f, kLo = 6.4206382432985265e-09f;
+  const float t = v * kHi;
+  float e = __builtin_fmaf(v, kHi, -t);
+  e = __builtin_fmaf(v, kLo, e);
+  const float u = __builtin_amdgcn_fractf(t) + e;
+  s = __builtin_amdgcn_sinf(u);
+  c = __builtin_amdgcn_cosf(u);
+}
+#ifndef CN_PE_HW
+#define CN_PE_HW 1
+#endif
+
 // shift the sign bit of v into the running mask word (one v_alignbit_b32)
 CN_DEV uint32_t push_sign(uint32_t bits, float v) {
   return __builtin_amdgcn_alignbit(bits, __builtin_bit_cast(uint32_t, v), 31);
@@ -364,11 +384,8 @@ struct Chain {
       const int comp = p % 3, oct = p / 3;
       const float v = (comp == 0 ? x[0] : comp == 1 ? x[1] : x[2]) * (float)(1 << oct);
       float sn, cs;
-#ifdef CN_FAST_PE
-      sn = __sinf(v); cs = __cosf(v);      // A/B measurement only: inaccurate for large |v|
-#else
-      sincosf(v, &sn, &cs);
-#endif
+      if constexpr (kBf16 && CN_PE_HW) sincos_turns(v, sn, cs);
+      else sincosf(v, &sn, &cs);
       pe[2 + 2 * k] = sn;
       pe[3 + 2 * k] = cs;
     }
@@ -381,7 +398,8 @@ struct Chain {
       if (p >= 0) {
         const int comp = p % 3, oct = p / 3;
         const float v = (comp == 0 ? d[0] : comp == 1 ? d[1] : d[2]) * (float)(1 << oct);
-        sincosf(v, &sn, &cs);
+        if constexpr (kBf16 && CN_PE_HW) sincos_turns(v, sn, cs);
+        else sincosf(v, &sn, &cs);
       }
       dp[2 + 2 * k] = sn;
       dp[3 + 2 * k] = cs;
@@ -612,8 +630,12 @@ struct Chain {
   }
 };
 
+// min waves per SIMD: 8-wave workgroups -> 2 (one workgroup per CU); bf16
+// 4-wave workgroups -> 2 (two workgroups per CU, so one's prologue and
+// epilogues run beside the other's MFMAs); fp32 4-wave -> 1 (512 VGPRs)
 template <int P, int SB, int TB, bool BWD, int WAVES, int MODE>
-__global__ __launch_bounds__(WAVES * 64, WAVES / 4) void chain_kernel(ChainArgs a) {
+__global__ __launch_bounds__(WAVES * 64, (WAVES >= 8 ? WAVES / 4 : (P == CN_P_BF16 ? 2 : 1))) void chain_kernel(
+    ChainArgs a) {
   Chain<P, SB, TB, BWD, WAVES, MODE>::run(a);
 }
 

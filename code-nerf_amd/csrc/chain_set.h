@@ -233,24 +233,34 @@ int db_setup(char* act, int act_M, int M, float* dbuf, char* ws, DbArgs* db) {
 template <int P, int SB, int TB>
 ChainSet make_chain_set() {
   using N = Net<SB, TB>;
-  constexpr int WAVES = P == CN_P_BF16 ? 8 : 4;
+#ifndef CN_FWD_WAVES
+#define CN_FWD_WAVES 8
+#endif
+#ifndef CN_BWD_WAVES
+#define CN_BWD_WAVES 8
+#endif
+  // bf16: 8-wave workgroups (two waves per SIMD, one workgroup per CU) by
+  // default; fp32 (bin operand of 144 VGPRs): 4 waves, one per SIMD
+  constexpr int WF = P == CN_P_BF16 ? CN_FWD_WAVES : 4;
+  constexpr int WB = P == CN_P_BF16 ? CN_BWD_WAVES : 4;
   ChainSet s;
   s.prec = P;
   s.SB = SB;
   s.TB = TB;
-  s.waves = WAVES;
-  s.tile = WAVES * 32;
+  s.waves_fwd = WF;
+  s.waves_bwd = WB;
+  s.tile = 256;
   s.n_params = ParamIdx{SB, TB}.count();
   s.n_inject = N::kInject;
   s.n_fwd_layers = N::kFwdLayers;
   s.pack_fwd_bytes = Sched<P, SB, TB, false>::packed_bytes();
   s.pack_bwd_bytes = Sched<P, SB, TB, true>::packed_bytes();
   s.blob_floats = BiasBlob<SB, TB>::kFloats;
-  s.fwd_train = chain_kernel<P, SB, TB, false, WAVES, CN_MODE_TRAIN>;
-  s.fwd_infer = chain_kernel<P, SB, TB, false, WAVES, CN_MODE_INFER>;
-  s.fwd_codes = chain_kernel<P, SB, TB, false, WAVES, CN_MODE_CODES>;
-  s.bwd = chain_kernel<P, SB, TB, true, WAVES, CN_MODE_TRAIN>;
-  s.bwd_codes = chain_kernel<P, SB, TB, true, WAVES, CN_MODE_CODES>;
+  s.fwd_train = chain_kernel<P, SB, TB, false, WF, CN_MODE_TRAIN>;
+  s.fwd_infer = chain_kernel<P, SB, TB, false, WF, CN_MODE_INFER>;
+  s.fwd_codes = chain_kernel<P, SB, TB, false, WF, CN_MODE_CODES>;
+  s.bwd = chain_kernel<P, SB, TB, true, WB, CN_MODE_TRAIN>;
+  s.bwd_codes = chain_kernel<P, SB, TB, true, WB, CN_MODE_CODES>;
   s.latent_fwd = latent_fwd_kernel<SB, TB>;
   s.latent_bwd = latent_bwd_kernel<SB, TB>;
   s.code_grad = code_grad_kernel<SB, TB>;

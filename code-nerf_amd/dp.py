@@ -121,6 +121,61 @@ class GradExchange:
         return {"model_all_reduce": self.bucket.flat.numel() * 4, "code_rows_all_gather": rows_per_rank * (1 + width) * 4}
 
 
+def world_rank(dist, group=None):
+    """(world, rank) of this process; (1, 0) without an initialised group."""
+    if dist is not None and dist.is_initialized():
+        return dist.get_world_size(group), dist.get_rank(group)
+    return 1, 0
+
+
+def shard(items, dist, group=None):
+    """This rank's share of ``items`` (round-robin, order kept): evaluation
+    views of src/optimizer.py:108-130 split across ranks."""
+    world, rank = world_rank(dist, group)
+    return list(items)[rank::world]
+
+
+def gather_by_key(local, dist, group=None):
+    """Merge every rank's {key: value} into one dict ordered by key, on every
+    rank (all_gather_object; no-op with one rank)."""
+    world, _ = world_rank(dist, group)
+    if world == 1:
+        return dict(sorted(local.items()))
+    parts = [None] * world
+    dist.all_gather_object(parts, dict(local), group=group)
+    merged = {}
+    for p in parts:
+        merged.update(p)
+    return dict(sorted(merged.items()))
+
+
+def ray_block(R, dist, group=None, align=1):
+    """Contiguous ray range [a, b) of this rank when one image is split into
+    row blocks (C5 inference); blocks are multiples of
+    ``align`` rays except the last."""
+    world, rank = world_rank(dist, group)
+    per = -(-R // world)
+    per = -(-per // align) * align
+    a = min(R, rank * per)
+    return a, min(R, a + per)
+
+
+def gather_ray_blocks(block, R, dist, group=None, align=1):
+    """Reassemble an image of R rays from every rank's ``block`` (rows
+    [a, b) of ray_block), on every rank."""
+    world, _ = world_rank(dist, group)
+    if world == 1:
+        return block
+    per = -(-R // world)
+    per = -(-per // align) * align
+    dev = torch.device("cpu") if dist.get_backend(group) == "gloo" else block.device
+    pad = torch.zeros((per,) + tuple(block.shape[1:]), dtype=block.dtype, device=dev)
+    pad[:block.shape[0]] = block.to(dev)
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad, group=group)
+    return torch.cat(parts)[:R].to(block.device)
+
+
 def object_for(step, rank, world, n_objects):
     """Object rendered by ``rank`` at global step ``step``: consecutive ranks
     take consecutive objects, so one step covers ``world`` distinct objects

@@ -12,7 +12,10 @@ save_img)``) and loop semantics:
     code regulariser on each view's chunk 0) accumulates gradients, then
     one AdamW step (:66-98);
   * evaluation: every view that is not a target, forward only, PSNR from the
-    mean of the chunk MSEs and SSIM (:108-130);
+    mean of the chunk MSEs and SSIM (:108-130); with torch.distributed the
+    views are split across ranks (dp.shard) and the metrics gathered
+    (dp.gather_by_key), the z jitter of every view drawn first in view order
+    so a split changes no draw;
   * ``codes.pth`` with the reference's keys (:138-145).
 The model weights are fixed, so the weight-gradient pass is skipped (only the
 dX chain and the code gradients run).  SSIM is ``metrics.ssim_legacy`` -- a
@@ -26,6 +29,7 @@ import time
 import numpy as np
 import torch
 
+from . import dp
 from .data import SRN, collate_one
 from .metrics import ssim_legacy
 from .model import CodeNeRF
@@ -37,11 +41,13 @@ from .utils import get_rays, image_float_to_uint8
 
 class Optimizer:
     def __init__(self, saved_dir, gpu=0, instance_ids=(), splits="test", jsonfile="srncar.json",
-                 batch_size=2048, num_opts=200, hpams=None, exp_root="exps"):
+                 batch_size=2048, num_opts=200, hpams=None, exp_root="exps", dist=None):
         self.hpams = hpams if hpams is not None else load_hpams(jsonfile)
         self.device = torch.device("cuda", int(gpu))
         torch.cuda.set_device(self.device)
         self.exp_root = exp_root
+        self.dist = dist
+        self.world, self.rank = dp.world_rank(dist)
         self.make_model()
         self.load_model_codes(saved_dir)
         self.make_dataloader(splits, len(instance_ids))
@@ -60,9 +66,10 @@ class Optimizer:
         return z.to(self.device)
 
     def optimize_objs(self, instance_ids, lr=1e-2, lr_half_interval=50, save_img=True):
-        with open(os.path.join(self.save_dir, "opt_hpams.json"), "w") as f:
-            json.dump({"instance_ids": list(map(int, instance_ids)), "lr": lr,
-                       "lr_half_interval": lr_half_interval, "": self.splits}, f, indent=2)
+        if self.rank == 0:
+            with open(os.path.join(self.save_dir, "opt_hpams.json"), "w") as f:
+                json.dump({"instance_ids": list(map(int, instance_ids)), "lr": lr,
+                           "lr_half_interval": lr_half_interval, "": self.splits}, f, indent=2)
         self.lr, self.lr_half_interval = lr, lr_half_interval
         instance_ids = [int(i) for i in instance_ids]
         n = len(self.dataset)
@@ -89,26 +96,33 @@ class Optimizer:
                     gts.append(tgt_img.reshape(H, W, 3))
                 self.opts.step()
                 self.log_opt_psnr(float(losses.mean()), time.time() - t1, num_obj)
-                if save_img:
+                if save_img and self.rank == 0:
                     self.save_img(gens, gts, self.ids[num_obj], self.nopts)
                 self.nopts += 1
                 if self.nopts % lr_half_interval == 0:
                     self.set_optimizers(shapecode, texturecode)
             with torch.no_grad():
-                for num in range(imgs.shape[1]):
-                    if num in instance_ids:
-                        continue
+                # evaluation views (src/optimizer.py:108-130), split across
+                # ranks when data parallel; the z jitter of every view is drawn
+                # first, in view order, so the split does not change any draw
+                views = [num for num in range(imgs.shape[1]) if num not in instance_ids]
+                zs = {num: self._z_vals() for num in views}
+                local = {}
+                for num in dp.shard(views, self.dist):
                     tgt_img = imgs[0, num].reshape(-1, 3).to(self.device)
                     rays_o, viewdir = get_rays(H, W, focal, poses[0, num])
-                    rgb, _ = self.step_impl.render(rays_o, viewdir, self._z_vals(), shapecode, texturecode)
+                    rgb, _ = self.step_impl.render(rays_o, viewdir, zs[num], shapecode, texturecode)
                     se = ((rgb - tgt_img) ** 2).sum(-1)
                     chunk_mse = [float(se[i:i + self.B].mean()) / 3 for i in range(0, H * W, self.B)]
-                    self.log_eval_psnr(float(np.mean(chunk_mse)), num_obj)
-                    self.ssim_eval.setdefault(num_obj, []).append(
-                        ssim_legacy(rgb.reshape(H, W, 3).cpu().numpy(), tgt_img.reshape(H, W, 3).cpu().numpy()))
+                    local[num] = (float(-10 * np.log(float(np.mean(chunk_mse))) / np.log(10)),
+                                  ssim_legacy(rgb.reshape(H, W, 3).cpu().numpy(),
+                                              tgt_img.reshape(H, W, 3).cpu().numpy()))
                     if save_img:
                         self.save_img([rgb.reshape(H, W, 3)], [tgt_img.reshape(H, W, 3)], self.ids[num_obj], num,
                                       opt=False)
+                for num, (psnr, ssim) in dp.gather_by_key(local, self.dist).items():
+                    self.psnr_eval.setdefault(num_obj, []).append(psnr)
+                    self.ssim_eval.setdefault(num_obj, []).append(ssim)
             self.optimized_shapecodes[num_obj] = shapecode.detach().cpu()
             self.optimized_texturecodes[num_obj] = texturecode.detach().cpu()
             self.save_opts(num_obj)
@@ -124,6 +138,8 @@ class Optimizer:
         self.psnr_eval.setdefault(num_obj, []).append(float(-10 * np.log(mse) / np.log(10)))
 
     def save_opts(self, num_obj):
+        if self.rank != 0:
+            return
         torch.save({"ids": [str(i) for i in self.ids], "num_obj": num_obj,
                     "optimized_shapecodes": self.optimized_shapecodes,
                     "optimized_texturecodes": self.optimized_texturecodes,
@@ -156,11 +172,18 @@ class Optimizer:
         self.mean_texture = torch.mean(saved["texture_code_params"]["weight"], dim=0).reshape(1, -1)
 
     def make_save_img_dir(self, save_dir):
-        tmp, num = save_dir, 2
-        while os.path.isdir(tmp):
-            tmp = save_dir + "_" + str(num)
-            num += 1
-        os.makedirs(tmp)
+        # rank 0 picks the first free "test", "test_2", ... and tells the others
+        tmp = None
+        if self.rank == 0:
+            tmp, num = save_dir, 2
+            while os.path.isdir(tmp):
+                tmp = save_dir + "_" + str(num)
+                num += 1
+            os.makedirs(tmp)
+        if self.world > 1:
+            box = [tmp]
+            self.dist.broadcast_object_list(box, src=0)
+            tmp = box[0]
         self.save_dir = tmp
 
     def make_dataloader(self, splits, num_instances_per_obj, crop_img=False):

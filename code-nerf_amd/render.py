@@ -21,6 +21,7 @@ stream while the weight-gradient pass of range i-1 runs on a side stream
 """
 import torch
 
+from . import dp as _dp
 from . import engine as _eng
 
 
@@ -304,3 +305,18 @@ class ImageStep:
         if len(rgbs) == 1:
             return rgbs[0], depths[0]
         return torch.cat(rgbs), torch.cat(depths)
+
+    @torch.no_grad()
+    def render_sharded(self, rays_o, viewdirs, z_vals, shape_code, texture_code, dist=None, group=None):
+        """One image rendered by all ranks (C5 inference):
+        rank r renders the contiguous ray block dp.ray_block(R, r) and the
+        blocks are all-gathered -> rgb (R,3), depth (R,) on every rank."""
+        R = rays_o.shape[0]
+        a, b = _dp.ray_block(R, dist, group)
+        z = z_vals if z_vals.dim() == 1 else z_vals[a:b]
+        if b > a:
+            rgb, depth = self.render(rays_o[a:b], viewdirs[a:b], z, shape_code, texture_code)
+        else:
+            rgb = torch.empty(0, 3, dtype=torch.float32, device=rays_o.device)
+            depth = torch.empty(0, dtype=torch.float32, device=rays_o.device)
+        return _dp.gather_ray_blocks(rgb, R, dist, group), _dp.gather_ray_blocks(depth, R, dist, group)

@@ -105,3 +105,95 @@ def test_object_assignment_covers_distinct_objects():
         for step in range(5):
             objs = [object_for(step, r, world, 64) for r in range(world)]
             assert len(set(objs)) == world
+
+
+# ---------------------------------------------------------------- evaluation / inference sharding
+def _eval_worker(rank, world, port, out):
+    """Evaluation views split across ranks (src/optimizer.py:108-130) and one
+    image rendered as contiguous ray blocks (C5 inference), with the oracle's
+    renderer standing in for the HIP one."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from codenerf_amd import dp
+    torch.set_num_threads(1)
+    p, st, tt, ro, vd, z, gts = _setup()
+    views = [0, 2, 3, 5, 6]
+
+    def view_metric(v):
+        with torch.no_grad():
+            xyz = ro[:, None, :] + vd[:, None, :] * (z + 0.01 * v)[:, None]
+            sig, rgb = ref_cpu.codenerf_forward(p, xyz, vd[:, None, :].expand(-1, NS, -1), st[v % N_OBJ][None],
+                                                tt[v % N_OBJ][None])
+            col, _ = ref_cpu.volume_rendering(sig, rgb, z)
+        return float(((col - gts[v % N_OBJ]) ** 2).mean())
+
+    local = {v: view_metric(v) for v in dp.shard(views, dist)}
+    merged = dp.gather_by_key(local, dist)
+    R = ro.shape[0]
+    a, b = dp.ray_block(R, dist, align=4)
+    with torch.no_grad():
+        xyz = ro[a:b, None, :] + vd[a:b, None, :] * z[:, None]
+        sig, rgb = ref_cpu.codenerf_forward(p, xyz, vd[a:b, None, :].expand(-1, NS, -1), st[1][None], tt[1][None])
+        col, _ = ref_cpu.volume_rendering(sig, rgb, z)
+    img = dp.gather_ray_blocks(col, R, dist, align=4)
+    if rank == 0:
+        out.put((merged, img.numpy(), sorted(local)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_eval_views_and_ray_blocks_sharded_match_single_process():
+    from codenerf_amd import dp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_eval_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    merged, img, mine = q.get(timeout=240)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    assert mine == [0, 3, 6]                       # round-robin share of rank 0
+    p, st, tt, ro, vd, z, gts = _setup()
+    views = [0, 2, 3, 5, 6]
+    ref = {}
+    for v in views:
+        with torch.no_grad():
+            xyz = ro[:, None, :] + vd[:, None, :] * (z + 0.01 * v)[:, None]
+            sig, rgb = ref_cpu.codenerf_forward(p, xyz, vd[:, None, :].expand(-1, NS, -1), st[v % N_OBJ][None],
+                                                tt[v % N_OBJ][None])
+            col, _ = ref_cpu.volume_rendering(sig, rgb, z)
+        ref[v] = float(((col - gts[v % N_OBJ]) ** 2).mean())
+    assert list(merged) == views and merged == ref
+    with torch.no_grad():
+        xyz = ro[:, None, :] + vd[:, None, :] * z[:, None]
+        sig, rgb = ref_cpu.codenerf_forward(p, xyz, vd[:, None, :].expand(-1, NS, -1), st[1][None], tt[1][None])
+        col, _ = ref_cpu.volume_rendering(sig, rgb, z)
+    np.testing.assert_allclose(img, col.numpy(), rtol=1e-6, atol=1e-7)
+
+
+def test_ray_blocks_cover_the_image():
+    from codenerf_amd import dp
+
+    class FakeDist:
+        def __init__(self, world, rank):
+            self.w, self.r = world, rank
+
+        def is_initialized(self):
+            return True
+
+        def get_world_size(self, group=None):
+            return self.w
+
+        def get_rank(self, group=None):
+            return self.r
+
+    for R in (1, 7, 36, 65536):
+        for world in (1, 2, 3, 8):
+            for align in (1, 4, 2048):
+                blocks = [dp.ray_block(R, FakeDist(world, r), align=align) for r in range(world)]
+                covered = [i for a, b in blocks for i in range(a, b)]
+                assert covered == list(range(R)), (R, world, align)

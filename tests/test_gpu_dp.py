@@ -125,3 +125,93 @@ def test_two_ranks_on_hip_match_summed_single_process():
     d = np.abs(res[0][0] - flat)
     assert d.max() <= 2 * STEPS * 1e-3 + 1e-6
     assert np.mean(d <= 1e-6 + 1e-4 * np.abs(flat)) > 0.99
+
+
+# ---------------------------------------------------------------- evaluation / inference sharding
+def _hp(root):
+    return {"net_hyperparams": {"shape_blocks": 3, "texture_blocks": 1, "W": 256, "num_xyz_freq": 10,
+                                "num_dir_freq": 4, "latent_dim": 256},
+            "data": {"cat": "srn_cars", "splits": "cars_train", "data_dir": root, "n_train_views": 4,
+                     "n_test_views": 7},
+            "N_samples": 16, "near": 0.8, "far": 1.8, "loss_reg_coef": 1e-4,
+            "lr_schedule": [{"type": "step", "lr": 1e-4, "interval": 3}, {"type": "step", "lr": 1e-3, "interval": 3}],
+            "check_points": 1000, "N_importance": 0, "precision": "fp32"}
+
+
+def _optimize(root, exps, dist=None):
+    from codenerf_amd.optimizer import Optimizer
+    opt = Optimizer("t", 0, [0], "test", hpams=_hp(root), batch_size=512, num_opts=2, exp_root=exps, dist=dist)
+    torch.manual_seed(7)
+    np.random.seed(7)
+    opt.optimize_objs([0], lr=1e-2, lr_half_interval=2, save_img=False)
+    return opt.psnr_eval, opt.ssim_eval
+
+
+def _shard_worker(rank, world, port, root, exps, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import torch.distributed as dist
+    from codenerf_amd import engine as _eng
+    from codenerf_amd.model import CodeNeRF
+    from codenerf_amd.render import ImageStep
+    from oracle.params import make_codes, make_params
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    psnr, ssim = _optimize(root, exps, dist)
+    # one 64x64 image rendered as two ray blocks
+    m = CodeNeRF(3, 1, precision="fp32")
+    m.load_state_dict({k: torch.tensor(v) for k, v in make_params(71).items()})
+    m = m.cuda()
+    c2w, _ = _scene(0)
+    ro, vd = _eng.get_rays_dev(64, 64, 65.6, True, c2w.cuda())
+    s, t = (torch.tensor(c[0], device="cuda") for c in make_codes(71, 1))
+    z = torch.linspace(0.8, 1.8, 32, device="cuda")
+    rgb, depth = ImageStep(m).render_sharded(ro, vd, z, s, t, dist)
+    q.put((rank, psnr, ssim, rgb.cpu().numpy(), depth.cpu().numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_ranks_shard_eval_views_and_ray_blocks(tmp_path):
+    """Optimizer evaluation views split across two ranks (src/optimizer.py:108-130)
+    give the single-process metrics; an image rendered as two ray blocks and
+    all-gathered equals the one-rank render bit for bit."""
+    import torch.multiprocessing as mp
+    from codenerf_amd import engine as _eng
+    from codenerf_amd.data import make_synthetic_srn
+    from codenerf_amd.model import CodeNeRF
+    from codenerf_amd.render import ImageStep
+    from codenerf_amd.trainer import Trainer
+    from oracle.params import make_codes, make_params
+    root, exps = str(tmp_path / "data"), str(tmp_path / "exps")
+    make_synthetic_srn(root, "srn_cars", "cars_train", n_obj=2, n_views=4, H=32, W=32, focal=32.8, seed=3)
+    make_synthetic_srn(root, "srn_cars", "cars_test", n_obj=1, n_views=7, H=32, W=32, focal=32.8, seed=4)
+    Trainer("t", 0, hpams=_hp(root), batch_size=512, check_iter=0, exp_root=exps).training(0, 2, 1)
+    psnr1, ssim1 = _optimize(root, exps)
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, root, exps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r[0], r[1:]) for r in (q.get(timeout=240) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert len(psnr1[0]) == 6                          # 7 views minus the target
+    for r in range(world):
+        assert res[r][0] == psnr1 and res[r][1] == ssim1
+    m = CodeNeRF(3, 1, precision="fp32")
+    m.load_state_dict({k: torch.tensor(v) for k, v in make_params(71).items()})
+    m = m.cuda()
+    c2w, _ = _scene(0)
+    ro, vd = _eng.get_rays_dev(64, 64, 65.6, True, c2w.cuda())
+    s, t = (torch.tensor(c[0], device="cuda") for c in make_codes(71, 1))
+    rgb, depth = ImageStep(m).render(ro, vd, torch.linspace(0.8, 1.8, 32, device="cuda"), s, t)
+    for r in range(world):
+        np.testing.assert_array_equal(res[r][2], rgb.cpu().numpy())
+        np.testing.assert_array_equal(res[r][3], depth.cpu().numpy())

@@ -65,14 +65,15 @@ def main():
     params = model.param_list()
     Mc = R * 64
     M = eng.pad(Mc) + R * 64
-    buf = step._ws[M]
+    buf = step._ws[eng.device]
+    cap = buf["cap"]
     blob, zvec = eng.latent_fwd(params, sc.detach()[0], tc.detach()[0])
     ro, vd = torch.rand(R, 3, device=dev), torch.nn.functional.normalize(torch.randn(R, 3, device=dev), dim=-1)
     ro = ro * 0.1 + torch.tensor([0.0, 0.4, 1.2], device=dev)
     z = torch.linspace(0.8, 1.8, 64, device=dev)
     out = {}
     if "fwd" in only:
-        t = timeit(lambda: eng.mlp_fwd(blob, Mc, rays_o=ro, rays_d=vd, z=z, n_samples=64, act=buf["act"], act_M=M,
+        t = timeit(lambda: eng.mlp_fwd(blob, Mc, rays_o=ro, rays_d=vd, z=z, n_samples=64, act=buf["act"], act_M=cap,
                                        act_row0=0, sigma=buf["sig"][:eng.pad(Mc)], rgb=buf["rgb"][:eng.pad(Mc)]),
                    a.reps)
         out["fwd_ms"] = round(t, 4)
@@ -80,12 +81,12 @@ def main():
         t = timeit(lambda: eng.mlp_fwd(blob, Mc, rays_o=ro, rays_d=vd, z=z, n_samples=64), a.reps)
         out["fwd_infer_ms"] = round(t, 4)
     if "bwd" in only:
-        t = timeit(lambda: eng.mlp_bwd(blob, M, buf["dsig"], buf["drgb"], buf["act"]), a.reps)
+        t = timeit(lambda: eng.mlp_bwd(blob, M, buf["dsig"], buf["drgb"], buf["act"], act_M=cap), a.reps)
         out["bwd_ms"] = round(t, 4)
         out["bwd_tflops"] = round(853_248 * M / t / 1e9, 1)
     if "dw" in only:
         grads = [torch.zeros_like(p) for p in params]
-        t = timeit(lambda: eng.mlp_dw(buf["act"], M, zvec, grads, buf["dbuf"], buf["dw"]), a.reps)
+        t = timeit(lambda: eng.mlp_dw(buf["act"], M, zvec, grads, buf["dbuf"], buf["dw"], act_M=cap), a.reps)
         out["dw_ms"] = round(t, 4)
         out["dw_tflops"] = round(899_328 * M / t / 1e9, 1)
         out["dw_alg_GBs"] = round(M * 250 * 1024 / 32 / t / 1e6, 1)
