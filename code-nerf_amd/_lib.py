@@ -48,6 +48,7 @@ _SIGS = {
     "cn_blob_floats": (_Z, [_P]),
     "cn_act_bytes": (_Z, [_P, _I]),
     "cn_dw_ws_bytes": (_Z, [_P, _I]),
+    "cn_act_plane": (ctypes.c_longlong, [_P, _I, _I, _I, ctypes.POINTER(_I)]),
     "cn_pack_weights": (_I, [_P, _P, _P, _P, _P]),
     "cn_latent_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P]),
     "cn_mlp_fwd": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _I, _I, _P]),
@@ -79,8 +80,14 @@ def load_library(path=LIB_PATH):
     if not os.path.exists(path):
         raise HipUnavailable(f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
     lib = ctypes.CDLL(path)
+    variant = os.path.abspath(path) != os.path.abspath(os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                                    LIB_NAME))
     for name, (res, args) in _SIGS.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:
+            if variant:          # an older A/B build may lack a newer query
+                continue
+            raise HipUnavailable(f"{path} does not export {name}")
         fn.restype = res
         fn.argtypes = args
     if lib.cn_abi_version() != ABI_VERSION:

@@ -122,6 +122,25 @@ size_t cn_act_bytes_per_sample(const cn_plan* p) {
 }
 size_t cn_dw_ws_bytes(const cn_plan* p, int M) { return p ? p->cs.dw_ws_bytes(M) : 0; }
 
+long long cn_act_plane(const cn_plan* p, int M, int kind, int index, int* width) {
+  if (!p || M <= 0 || M > CN_MAX_SAMPLES) return -1;
+  const ActLayout L = p->cs.layout(cn_pad_samples(p, M));
+  int w = 0;
+  long long off = -1;
+  if ((kind == CN_PLANE_Y || kind == CN_PLANE_DA) && index >= 0 && index < kMaxPlanes) {
+    w = (int)(kind == CN_PLANE_Y ? L.Yw[index] : L.dAw[index]);
+    if (w > 0) off = (long long)(kind == CN_PLANE_Y ? L.Y[index] : L.dA[index]);
+  } else if (kind == CN_PLANE_PE) {
+    w = 64, off = (long long)L.pe;
+  } else if (kind == CN_PLANE_DIR) {
+    w = 32, off = (long long)L.dir;
+  } else if (kind == CN_PLANE_MASKS) {
+    w = (int)(L.mask_bytes_per_slab / 32), off = (long long)L.masks;
+  }
+  if (width) *width = w;
+  return off;
+}
+
 int cn_pack_weights(const cn_plan* p, const float* const* d_params, void* d_fwd, void* d_bwd, void* stream) {
   if (!p || !d_params) return fail("cn_pack_weights: NULL argument");
   if (!p->d_fwd_idx && upload_tables(const_cast<cn_plan*>(p))) return -1;

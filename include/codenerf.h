@@ -65,6 +65,16 @@ size_t cn_packed_bytes(const cn_plan *plan, int bwd); /* packed weights */
 size_t cn_blob_floats(const cn_plan *plan);         /* per-call bias blob */
 size_t cn_act_bytes(const cn_plan *plan, int M);    /* training activations */
 size_t cn_dw_ws_bytes(const cn_plan *plan, int M);  /* weight-grad partials */
+/* Layout introspection of the training workspace laid out for M samples
+ * (tests and debugging): byte offset of a plane (-1 if it does not exist);
+ * *width = its elements per sample (masks: bytes per sample).  Plane
+ * element layout: code-nerf_amd/csrc/cn_layout.h (slab_off / plane_off). */
+#define CN_PLANE_Y 0     /* index: forward layer whose output it is */
+#define CN_PLANE_DA 1    /* index: forward layer whose pre-activation gradient it is */
+#define CN_PLANE_PE 2
+#define CN_PLANE_DIR 3
+#define CN_PLANE_MASKS 4
+long long cn_act_plane(const cn_plan *plan, int M, int kind, int index, int *width);
 
 /* ---- weights: pack the parameters into the chain kernels' fragment order
  * (fwd: W, bwd: W^T).  Call after every optimiser step. */
