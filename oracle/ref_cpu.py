@@ -74,7 +74,50 @@ def positional_encoding(x, n_freq):
     return torch.cat([x, torch.sin(y), torch.cos(y)], -1)
 
 
+# ---- the bf16 kernels' operand precision, restated (chain.hip / dw.hip with
+# CN_BF16): every per-sample Linear multiplies bf16-rounded inputs by
+# bf16-rounded weights with fp32 accumulation and an fp32 bias; the backward
+# uses bf16-rounded upstream gradients (the stored dA planes) against the
+# bf16 weights (dX) and the bf16 inputs (dW).  The per-object latent layers
+# and the sigma head run in fp32 there (latent.hip; the sigma head reads the
+# fp32 accumulator), so they stay fp32 here.  Off by default: the oracle is
+# the fp32 reference; ``bf16_operands()`` switches a block of code over.
+_BF16 = {"on": False}
+
+
+def _rb(t):
+    return t.to(torch.bfloat16).to(torch.float32)
+
+
+class _Bf16Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        xb, wb = _rb(x), _rb(w)
+        ctx.save_for_backward(xb, wb)
+        return xb @ wb.t() + b
+
+    @staticmethod
+    def backward(ctx, dy):
+        xb, wb = ctx.saved_tensors
+        d = _rb(dy)
+        d2, x2 = d.reshape(-1, d.shape[-1]), xb.reshape(-1, xb.shape[-1])
+        return d @ wb, d2.t() @ x2, d2.sum(0)
+
+
+class bf16_operands:
+    """with ref_cpu.bf16_operands(): ... -- the bf16 kernels' arithmetic."""
+
+    def __enter__(self):
+        self.prev = _BF16["on"]
+        _BF16["on"] = True
+
+    def __exit__(self, *exc):
+        _BF16["on"] = self.prev
+
+
 def _lin(p, name, x):
+    if _BF16["on"] and "latent" not in name and not name.startswith("sigma"):
+        return _Bf16Linear.apply(x, p[name + ".weight"], p[name + ".bias"])
     return F.linear(x, p[name + ".weight"], p[name + ".bias"])
 
 

@@ -90,3 +90,23 @@ def test_train_step_grads_and_adamw(case):
                                    rtol=1e-6, atol=1e-8)
     np.testing.assert_allclose(r["shape_table"].detach().numpy(), g["adamw/shape_table"], rtol=1e-6, atol=1e-8)
     np.testing.assert_allclose(r["texture_table"].detach().numpy(), g["adamw/texture_table"], rtol=1e-6, atol=1e-8)
+
+
+def test_bf16_operand_mode_is_scoped_and_close():
+    """ref_cpu.bf16_operands() restates the bf16 kernels' operand rounding;
+    outside the block the oracle is the fp32 reference again."""
+    import torch
+    from oracle import ref_cpu
+    from oracle.params import make_params, make_codes
+    p = ref_cpu.param_tensors(make_params(2), requires_grad=False)
+    s, t = (torch.tensor(c) for c in make_codes(2, 1))
+    g = torch.Generator().manual_seed(0)
+    x = torch.rand(64, 8, 3, generator=g) * 2 - 1
+    v = torch.nn.functional.normalize(torch.randn(64, 8, 3, generator=g), dim=-1)
+    s32, r32 = ref_cpu.codenerf_forward(p, x, v, s, t)
+    with ref_cpu.bf16_operands():
+        s16, r16 = ref_cpu.codenerf_forward(p, x, v, s, t)
+    s32b, r32b = ref_cpu.codenerf_forward(p, x, v, s, t)
+    assert torch.equal(s32, s32b) and torch.equal(r32, r32b)
+    assert not torch.equal(r16, r32)
+    assert float((r16 - r32).abs().max()) < 5e-3
