@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--dw-side-wgs", type=int, default=None,
                     help="persistent workgroups of the dW launches that run beside a dX chain (0: 256)")
     ap.add_argument("--no-fp32", action="store_true", help="skip the secondary fp32 figure of the C2 step")
+    ap.add_argument("--recompute", action="store_true",
+                    help="store-vs-recompute A/B: loss forwards store masks only, a second forward writes the dW planes")
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="CPU baseline threads (default: OMP_NUM_THREADS, else all host CPUs)")
     # rehearsal of the N > 1 path on a one-GPU box: gloo, every rank on cuda:0
@@ -137,6 +139,7 @@ def build_workload(args, dev, rank, world, precision, timers, dist):
     core = TrainCore(model, shape_codes, texture_codes, near=near, far=far, n_coarse=args.n_coarse,
                      n_fine=args.n_fine, chunk=2048, reg_coef=1e-4, lr=(1e-4, 1e-3), timers=timers,
                      dist=dist, step_opts=opts)
+    core.step_impl.recompute = bool(getattr(args, "recompute", False))
     # synthetic views: a ray-cast ellipsoid object per rank (the SRN-format
     # generator's renderer, data.make_synthetic_srn) from poses on the sphere
     import numpy as np

@@ -40,6 +40,9 @@ class ImageStep:
         self.dw_side_wgs = int(dw_side_wgs)      # workgroups of the overlapped dW launches (0: one per CU)
         self.act_budget = act_budget
         self.max_rays = max_rays                 # explicit cap on rays per part (tests)
+        # store-vs-recompute A/B (fine step only): the loss forwards store no
+        # dW operand planes; a second forward writes them before the backward
+        self.recompute = False
         self._ws = {}                            # device -> grow-only workspace
         self._side = {}                          # device -> side stream
 
@@ -62,6 +65,9 @@ class ImageStep:
                       rgb=torch.empty(cap, 3, dtype=torch.float32, device=dev),
                       dsig=torch.empty(cap, dtype=torch.float32, device=dev),
                       drgb=torch.empty(cap, 3, dtype=torch.float32, device=dev))
+            if self.recompute:      # outputs of the recompute forward (discarded)
+                ws.update(dsig_tmp=torch.empty(cap, dtype=torch.float32, device=dev),
+                          drgb_tmp=torch.empty(cap, 3, dtype=torch.float32, device=dev))
             self._ws[eng.device] = ws
         return ws
 
@@ -253,9 +259,10 @@ class ImageStep:
         blob, zvec = eng.latent_fwd(params, s, t)
         tm = self.timers
         ev = tm.mark("fwd") if tm else None
+        rc = self.recompute
         sig_c, rgb_c = eng.mlp_fwd(blob, Mc, rays_o=rays_o, rays_d=viewdirs, z=z_c,
                                    z_stride=0 if z_c.dim() == 1 else Nc, n_samples=Nc, act=ws["act"], act_M=cap,
-                                   act_row0=0, sigma=sig[:Mc_p], rgb=rgb[:Mc_p])
+                                   act_row0=0, sigma=sig[:Mc_p], rgb=rgb[:Mc_p], codes=rc)
         if tm:
             tm.done("fwd", ev)
         _, loss_c, _, _ = _eng.render_loss(sig_c, rgb_c, z_c, R, Nc, gt, self.chunk, self.white_bg,
@@ -267,12 +274,24 @@ class ImageStep:
         ev = tm.mark("fwd") if tm else None
         sig_f, rgb_f = eng.mlp_fwd(blob, Mf, rays_o=rays_o, rays_d=viewdirs, z=z_f, z_stride=Nf, n_samples=Nf,
                                    act=ws["act"], act_M=cap, act_row0=Mc_p, sigma=sig[Mc_p:Mp],
-                                   rgb=rgb[Mc_p:Mp])
+                                   rgb=rgb[Mc_p:Mp], codes=rc)
         if tm:
             tm.done("fwd", ev)
         out_f, loss_f = _eng.render_loss_fine(sig_c, rgb_c, z_c, Nc, sig_f, rgb_f, z_f, Nf, R, gt, self.chunk,
                                               dsig[:Mc], drgb[:Mc], dsig[Mc_p:Mc_p + Mf],
                                               drgb[Mc_p:Mc_p + Mf], self.white_bg)
+        if rc:
+            # recompute A/B (hard part 2): the forward passes above
+            # stored only ReLU masks + sigma pre-activations; the planes the dW
+            # pass reads are produced here by a second training forward
+            ev = tm.mark("fwd") if tm else None
+            eng.mlp_fwd(blob, Mc, rays_o=rays_o, rays_d=viewdirs, z=z_c, z_stride=0 if z_c.dim() == 1 else Nc,
+                        n_samples=Nc, act=ws["act"], act_M=cap, act_row0=0, sigma=ws["dsig_tmp"][:Mc_p],
+                        rgb=ws["drgb_tmp"][:Mc_p])
+            eng.mlp_fwd(blob, Mf, rays_o=rays_o, rays_d=viewdirs, z=z_f, z_stride=Nf, n_samples=Nf, act=ws["act"],
+                        act_M=cap, act_row0=Mc_p, sigma=ws["dsig_tmp"][Mc_p:Mp], rgb=ws["drgb_tmp"][Mc_p:Mp])
+            if tm:
+                tm.done("fwd", ev)
         self._bwd_dw(eng, blob, ws, zvec, eng.table(grads), M)
         reg_out = torch.zeros(1, dtype=torch.float32, device=eng.device)
         eng.latent_bwd(params, grads, s, t, zvec, ws["dbuf"], shape_table.grad[obj_idx],

@@ -177,3 +177,31 @@ def test_overlapped_bwd_dw_matches_single_pass(precision, case, Nf):
     for i in (1, 2):
         x, y = a[i].grad.cpu().numpy(), b[i].grad.cpu().numpy()
         np.testing.assert_allclose(x, y, rtol=1e-4, atol=1e-5 * max(1e-30, np.abs(y).max()))
+
+
+def test_recompute_schedule_matches_store_schedule():
+    """The store-vs-recompute A/B (ImageStep.recompute: loss forwards keep only
+    masks, a second forward writes the dW operand planes) computes the same
+    step bit for bit -- it differs only in time."""
+    g = load("n64_16x16")
+    R = g["rays_o"].shape[0]
+    rnd = torch.rand(R, 64, generator=torch.Generator().manual_seed(12))
+    outs = []
+    for rc in (False, True):
+        from codenerf_amd.model import CodeNeRF
+        from codenerf_amd.render import ImageStep
+        m = CodeNeRF(3, 1, precision="bf16")
+        m.load_state_dict({k: torch.tensor(v) for k, v in case_params(g).items()})
+        m = m.to(_dev())
+        st = torch.nn.Parameter(torch.tensor(g["shape_table"], device=_dev()))
+        tt = torch.nn.Parameter(torch.tensor(g["texture_table"], device=_dev()))
+        step = ImageStep(m, chunk=int(g["chunk"]), reg_coef=1e-4)
+        step.recompute = rc
+        lc, lf, rgb, _ = step.forward_backward_fine(torch.tensor(g["rays_o"], device=_dev()),
+                                                    torch.tensor(g["viewdir"], device=_dev()),
+                                                    torch.tensor(g["z_vals"], device=_dev()), rnd.to(_dev()),
+                                                    torch.tensor(g["gt"], device=_dev()), st, tt, int(g["obj_idx"]))
+        torch.cuda.synchronize()
+        outs.append([lf.cpu(), rgb.cpu()] + [p.grad.cpu() for p in m.parameters()] + [st.grad.cpu()])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

@@ -12,7 +12,7 @@ TAG=$1
 shift
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
-BENCH="bench.py --no-cpu-baseline --steps 5 --warmup 2 $*"
+BENCH="bench.py --no-cpu-baseline --no-fp32 --steps 20 --warmup 5 $*"
 
 run() {
   "$@"

@@ -24,13 +24,16 @@ N_SIMD = 1024      # 256 CUs x 4
 N_XCD = 8
 
 
-def short(name):
+def short(name, prec):
     m = re.search(r"chain_kernel<(\d), \d, \d, (true|false), \d+, (\d)>", name)
+    if m and int(m.group(1)) != prec:
+        return None
     if m:
         mode = int(m.group(3))
         kind = "bwd" if m.group(2) == "true" else "fwd"
         return kind if mode == 1 else f"{kind}_codes" if mode == 2 else f"{kind}_infer"
-    if re.search(r"\bdw_kernel<\d>", name):
+    m = re.search(r"\bdw_kernel<(\d)>", name)
+    if m and int(m.group(1)) == prec:
         return "dw"
     return None
 
@@ -89,7 +92,7 @@ def main():
         lines.append(f"| `{name[:90]}` | {r['Calls']} | {avg_ns / 1e3:.1f} | {float(r['Percentage']):.2f} | "
                      f"{fmt(hbm and hbm / 1e9, 3)} | {fmt(gbs, 1)} | {fmt(tfl, 4)} | {fmt(pmc_ns and pmc_ns / 1e3, 1)} | "
                      f"{fmt(util, 3)} | {fmt(clk, 2)} |")
-        s = short(name)
+        s = short(name, 0 if config == "c5" else 1)
         if s and hbm:
             traffic[s] = {"hbm_bytes": int(hbm), "fetch_kib": f, "write_kib": w, "avg_ns": avg_ns,
                           "mfma_util": util, "eff_clock_ghz": clk, "pmc_pass_avg_ns": pmc_ns, "mfma_flop": mops * 512 if mops else None,
