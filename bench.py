@@ -33,7 +33,7 @@ BF16_PEAK_TFLOPS = 2500.0       # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 FP32_PEAK_TFLOPS = 157.3        # fp32 MFMA
 HBM_PEAK_GBS = 8000.0
 FLOP_PER_SAMPLE = {"fwd": 899_328, "bwd": 853_248, "dw": 899_328}
-DW_BYTES_PER_SAMPLE = 8_000     # bf16 dA + X operand planes read by dw_kernel
+DW_BYTES_PER_SAMPLE = 6_976     # bf16 dA + X operand planes read by dw_kernel (encoding_shape folded)
 
 
 def parse():

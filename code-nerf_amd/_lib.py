@@ -55,9 +55,9 @@ _SIGS = {
     "cn_mlp_bwd": (_I, [_P, _P, _P, _I, _P, _P, _P, _P]),
     "cn_mlp_fwd_codes": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _I, _I, _P]),
     "cn_mlp_bwd_codes": (_I, [_P, _P, _P, _I, _P, _P, _P, _I, _I, _P]),
-    "cn_mlp_dw": (_I, [_P, _P, _I, _P, _P, _P, _P, _P]),
+    "cn_mlp_dw": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P]),
     "cn_mlp_bwd_rows": (_I, [_P, _P, _P, _I, _P, _P, _P, _I, _I, _P]),
-    "cn_mlp_dw_rows": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _I, _I, _P, _P]),
+    "cn_mlp_dw_rows": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _P, _P]),
     "cn_mlp_dbias": (_I, [_P, _P, _I, _I, _P, _P, _P]),
     "cn_latent_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P]),
     "cn_get_rays": (_I, [_I, _I, _D, _I, _P, _P, _P, _P]),

@@ -294,8 +294,9 @@ int cn_mlp_bwd_codes(const cn_plan* p, const void* d_pack, const float* d_blob, 
 }
 
 static int mlp_dw_impl(const cn_plan* p, void* d_act, int act_M, int act_row0, int M, const float* d_zvec,
-                       float* const* d_grads, float* d_dbuf, int db_accum, int nwg_req, void* d_ws, void* stream) {
-  if (!p || !d_act || !d_zvec || !d_grads || !d_dbuf || !d_ws) return fail("cn_mlp_dw: NULL argument");
+                       const float* const* d_params, float* const* d_grads, float* d_dbuf, int db_accum, int nwg_req,
+                       void* d_ws, void* stream) {
+  if (!p || !d_act || !d_zvec || !d_params || !d_grads || !d_dbuf || !d_ws) return fail("cn_mlp_dw: NULL argument");
   if (check_samples(M, "cn_mlp_dw")) return -1;
   if (act_M <= 0) act_M = M;
   if (check_samples(act_M, "cn_mlp_dw (act_M)")) return -1;
@@ -312,18 +313,25 @@ static int mlp_dw_impl(const cn_plan* p, void* d_act, int act_M, int act_row0, i
   else hipLaunchKernelGGL(dw_kernel<CN_P_FP32>, dim3(nwg), dim3(512), 0, S(stream), dw);
   if (launch_check("dw_kernel")) return -1;
   hipLaunchKernelGGL(dw_reduce_kernel, dim3(grid_for(red.prefix[red.nprob], 256)), dim3(256), 0, S(stream), red);
-  return launch_check("dw_reduce_kernel");
+  if (launch_check("dw_reduce_kernel")) return -1;
+  DwFoldArgs f = p->cs.fold_args();
+  f.fold = red.fold;
+  f.params = d_params;
+  f.grads = d_grads;
+  hipLaunchKernelGGL(dw_fold_kernel, dim3(9, 9, 2), dim3(256), 0, S(stream), f);
+  return launch_check("dw_fold_kernel");
 }
 
-int cn_mlp_dw(const cn_plan* p, void* d_act, int M, const float* d_zvec, float* const* d_grads, float* d_dbuf,
-              void* d_ws, void* stream) {
-  return mlp_dw_impl(p, d_act, M, 0, M, d_zvec, d_grads, d_dbuf, 0, 0, d_ws, stream);
+int cn_mlp_dw(const cn_plan* p, void* d_act, int M, const float* d_zvec, const float* const* d_params,
+              float* const* d_grads, float* d_dbuf, void* d_ws, void* stream) {
+  return mlp_dw_impl(p, d_act, M, 0, M, d_zvec, d_params, d_grads, d_dbuf, 0, 0, d_ws, stream);
 }
 
 int cn_mlp_dw_rows(const cn_plan* p, void* d_act, int act_M, int act_row0, int M, const float* d_zvec,
-                   float* const* d_grads, float* d_dbuf, int db_accum, int n_workgroups, void* d_ws,
-                   void* stream) {
-  return mlp_dw_impl(p, d_act, act_M, act_row0, M, d_zvec, d_grads, d_dbuf, db_accum, n_workgroups, d_ws, stream);
+                   const float* const* d_params, float* const* d_grads, float* d_dbuf, int db_accum,
+                   int n_workgroups, void* d_ws, void* stream) {
+  return mlp_dw_impl(p, d_act, act_M, act_row0, M, d_zvec, d_params, d_grads, d_dbuf, db_accum, n_workgroups, d_ws,
+                     stream);
 }
 
 int cn_mlp_dbias(const cn_plan* p, void* d_act, int act_M, int M, float* d_dbuf, void* d_ws, void* stream) {

@@ -185,7 +185,8 @@ struct Chain {
   // dA of the first forward layer) has no next layer and is stored in place.
   static constexpr bool codes_plane(int p) { return MODE == CN_MODE_CODES && p >= 1 && N::fwd(p - 1).inj >= 0; }
   static constexpr bool plane_of(int i) {
-    return BWD ? (PLANES || codes_plane(S::L(i).plane)) : (PLANES && S::L(i).plane >= 0);
+    const int p = S::L(i).plane;
+    return BWD ? ((PLANES && N::stored(p)) || codes_plane(p)) : (PLANES && p >= 0 && N::stored(p));
   }
   static constexpr bool defers(int i) { return kBf16 && plane_of(i) && i + 1 < NL; }
   static constexpr int deferred_count(int i) { return defers(i) ? 2 * S::L(i).T : 0; }

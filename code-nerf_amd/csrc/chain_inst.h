@@ -10,6 +10,7 @@ namespace cn {
 
 struct DwArgs;
 struct DwRedArgs;
+struct DwFoldArgs;
 struct DbArgs;
 struct LatentArgs;
 struct LatentBwdArgs;
@@ -42,6 +43,8 @@ struct ChainSet {
   int (*dw_setup)(char* act, int act_M, int row0, int M, int nwg, const float* zvec, float* dbuf, char* ws,
                   DwArgs* dw, DwRedArgs* red) = nullptr;
   size_t (*dw_ws_bytes)(int M) = nullptr;
+  // parameter indices of the encoding_shape fold (dw_fold_kernel)
+  DwFoldArgs (*fold_args)() = nullptr;
   // fills the bias-only argument block (dbuf rows of the injection layers)
   int (*db_setup)(char* act, int act_M, int M, float* dbuf, char* ws, DbArgs* db) = nullptr;
 };

@@ -81,12 +81,13 @@ ActLayout act_layout(size_t Mp) {
   auto take = [&](size_t n) { size_t o = off; off += (n + 255) & ~(size_t)255; return o; };
   L.pe = take(Mp * 64 * es);
   L.dir = take(Mp * 32 * es);
+  // planes the kernels do not write (N::stored) take no space: width 0
   for (int p = 0; p < N::kPlanes; ++p) {
-    L.Yw[p] = N::plane_width(p);
+    L.Yw[p] = N::stored(p) ? N::plane_width(p) : 0;
     L.Y[p] = take(Mp * L.Yw[p] * es);
   }
   for (int p = 0; p < N::kPlanes; ++p) {
-    L.dAw[p] = N::dplane_width(p);
+    L.dAw[p] = N::stored(p) ? N::dplane_width(p) : 0;
     L.dA[p] = take(Mp * L.dAw[p] * es);
   }
   L.d8 = take(Mp * 32 * es);
@@ -102,9 +103,13 @@ ActLayout act_layout(size_t Mp) {
 // Fewer workgroups leave CUs to a dX chain running beside the dW pass.
 constexpr int kDwWorkgroups = 256;
 
+constexpr size_t dw_part_bytes() {
+  return (size_t)kDwWorkgroups * 2 * ((size_t)kPartRows * kPartCols + kPartRows) * sizeof(float);
+}
+
 template <int P, int SB, int TB>
 size_t dw_ws_bytes(int) {
-  return (size_t)kDwWorkgroups * 2 * ((size_t)kPartRows * kPartCols + kPartRows) * sizeof(float);
+  return dw_part_bytes() + (size_t)kFoldRows * kFoldCols * sizeof(float);   // + the fold operand Gx
 }
 
 // Rows [row0, row0 + pad(M)) of a workspace laid out for act_M samples
@@ -121,23 +126,32 @@ int dw_setup(char* act, int act_M, int row0, int M, int nwg_req, const float* zv
   if (row0 < 0 || row0 % 256 || row0 + Mp > Ma) return -1;
   const ActLayout A = act_layout<P, SB, TB>(Ma);
   const size_t r0 = (size_t)row0 * ES;      // byte offset per element of plane width
-  static_assert(N::kFwdLayers <= kDwMaxProblems, "dw problems");
+  static_assert(N::kFwdLayers - 1 <= kDwMaxProblems, "dw problems");
+  static_assert(!N::stored(SB + 1) && N::stored(SB), "the fold assumes encoding_shape's planes are the unstored ones");
   *dw = DwArgs{};
   *red = DwRedArgs{};
-  dw->nprob = red->nprob = N::kFwdLayers;
+  // one problem per forward layer except encoding_shape (L = SB + 1), whose
+  // gradients come out of the viewdir problem's fold (dw_fold_kernel)
+  constexpr int NP = N::kFwdLayers - 1;
+  auto layer_of = [](int k) { return k <= SB ? k : k + 1; };
+  dw->nprob = red->nprob = NP;
   dw->total_tiles = Mp / 32;
   int ep = 0;
   long long wsum = 0, min_total = -1;
-  for (int L = 0; L < N::kFwdLayers; ++L) {
+  for (int k = 0; k < NP; ++k) {
+    const int L = layer_of(k);
     const bool last = L == N::kFwdLayers - 1;
     const bool vd = L == SB + 2;
-    DwProblem& p = dw->p[L];
+    DwProblem& p = dw->p[k];
     p.a_width = last ? 32 : N::dplane_width(L);
     p.A = act + (last ? A.d8 : A.dA[L]) + r0 * p.a_width;
     p.a_tiles = p.a_width / 32;
     p.out_tiles = last ? 1 : N::fwd(L).T;
+    // viewdir: X = Y of the last shape layer (encoding_shape's INPUT), the fold
+    // maps the accumulated dA_viewdir (x) Y_shape through encoding_shape
+    const int xin = vd ? SB : L - 1;
     if (L == 0) { p.X0 = act + A.pe + r0 * 64; p.x0_width = 64; }
-    else { p.x0_width = N::plane_width(L - 1); p.X0 = act + A.Y[L - 1] + r0 * p.x0_width; }
+    else { p.x0_width = N::plane_width(xin); p.X0 = act + A.Y[xin] + r0 * p.x0_width; }
     p.x0_tiles = p.x0_width / 32;
     if (vd) { p.X1 = act + A.dir + r0 * 32; p.x1_width = 32; p.x1_tiles = 1; }
     p.sigma_head = vd ? 1 : 0;
@@ -148,13 +162,13 @@ int dw_setup(char* act, int act_M, int row0, int M, int nwg_req, const float* zv
       const int* e = shape[p.kind];
       if (p.a_tiles != e[0] || p.x0_tiles != e[1] || p.x1_tiles != e[2] || p.out_tiles != e[3]) return -1;
     }
-    dw->pbytes[L] = (p.a_tiles + p.x0_tiles + p.x1_tiles) * 1024 * ES;
-    dw->wprefix[L] = wsum;
-    const long long tot = (long long)dw->pbytes[L] * dw->total_tiles;
+    dw->pbytes[k] = (p.a_tiles + p.x0_tiles + p.x1_tiles) * 1024 * ES;
+    dw->wprefix[k] = wsum;
+    const long long tot = (long long)dw->pbytes[k] * dw->total_tiles;
     wsum += tot;
     if (min_total < 0 || tot < min_total) min_total = tot;
 
-    DwRedProblem& r = red->p[L];
+    DwRedProblem& r = red->p[k];
     r.out_real = last ? 3 : N::fwd(L).T * 32;
     r.in_real = real_in_width<SB>(L, TB);
     r.cols = (p.x0_tiles + p.x1_tiles) * 32;
@@ -167,40 +181,61 @@ int dw_setup(char* act, int act_M, int row0, int M, int nwg_req, const float* zv
     r.z = inj >= 0 ? zvec + inj * 256 : nullptr;
     r.dbout = inj >= 0 ? dbuf + inj * 256 : nullptr;
     r.elems = (r.out_real + (vd ? 1 : 0)) * r.cols;
-    r.pbytes = dw->pbytes[L];
-    red->prefix[L] = ep;
+    r.pbytes = dw->pbytes[k];
+    red->prefix[k] = ep;
     ep += r.elems;
-    red->wprefix[L] = dw->wprefix[L];
+    red->wprefix[k] = dw->wprefix[k];
   }
-  dw->wprefix[N::kFwdLayers] = red->wprefix[N::kFwdLayers] = wsum;
-  red->prefix[N::kFwdLayers] = ep;
+  dw->wprefix[NP] = red->wprefix[NP] = wsum;
+  red->prefix[NP] = ep;
   // a share (wsum / nwg bytes) never exceeds the smallest problem, so it
   // holds slabs of at most two problems
   const long long nwg = nwg_req > 0 ? std::min(nwg_req, kDwWorkgroups) : kDwWorkgroups;
   if ((wsum + min_total - 1) / min_total >= nwg) return -1;
   dw->nwg = red->nwg = (int)nwg;
   // which partial slots hold each problem (the kernel's own segment walk)
-  for (int L = 0; L < N::kFwdLayers; ++L) red->gfirst[L] = -1;
+  for (int k = 0; k < NP; ++k) red->gfirst[k] = -1;
   for (int g = 0; g < (int)nwg; ++g) {
     const long long b0 = dw_share_begin(g, wsum, (int)nwg), b1 = dw_share_begin(g + 1, wsum, (int)nwg);
     int seg = 0;
-    for (int L = 0; L < N::kFwdLayers && seg < 2; ++L) {
+    for (int k = 0; k < NP && seg < 2; ++k) {
       int t0, t1;
-      dw_slab_range(dw->wprefix, dw->pbytes, dw->total_tiles, L, b0, b1, t0, t1);
+      dw_slab_range(dw->wprefix, dw->pbytes, dw->total_tiles, k, b0, b1, t0, t1);
       if (t1 <= t0) continue;
-      if (red->gfirst[L] < 0) { red->gfirst[L] = g; red->gseg[L] = seg; }
+      if (red->gfirst[k] < 0) { red->gfirst[k] = g; red->gseg[k] = seg; }
       else if (seg != 0) return -1;      // only a problem's first workgroup may hold it second
-      red->glast[L] = g;
+      red->glast[k] = g;
       ++seg;
     }
   }
-  for (int L = 0; L < N::kFwdLayers; ++L)
-    if (red->gfirst[L] < 0) return -1;
+  for (int k = 0; k < NP; ++k)
+    if (red->gfirst[k] < 0) return -1;
   dw->part = (float*)ws;
   dw->dbpart = (float*)(ws + (size_t)kDwWorkgroups * 2 * kPartRows * kPartCols * sizeof(float));
   red->part = dw->part;
   red->dbpart = dw->dbpart;
+  red->fold = (float*)(ws + dw_part_bytes());
   return (int)nwg;
+}
+
+// The encoding_shape fold (see Net::stored): the viewdir problem accumulates
+// Gx[n][k] = sum_m dA_vd[m][n] * Y_s[m][k] with Y_s the last shape layer's
+// output (n < 256: viewdir rows, n = 256: the sigma head), plus column
+// k = 256 = sum_m dA_vd[m][n] (the bias gradients).  encoding_shape is
+// Y_e = W_e Y_s + b_e, so with Wx_e = [W_e | b_e] (256 x 257) and
+// Wx_v[n][f] = W_v[n][f] (n < 256, the y columns of encoding_viewdir) or
+// w_sigma[f] (n = 256):
+//   d[W_v y-part ; w_sigma][n][f] = sum_k Gx[n][k] Wx_e[f][k]
+//   d[W_e | b_e][f][k]            = sum_n Wx_v[n][f] Gx[n][k]
+template <int SB, int TB>
+DwFoldArgs fold_args() {
+  constexpr ParamIdx PI{SB, TB};
+  DwFoldArgs f{};
+  f.w_shape = PI.enc_shape_w();
+  f.w_view = PI.viewdir_w();
+  f.view_cols = real_in_width<SB>(SB + 2, TB);
+  f.w_sigma = PI.sigma_w();
+  return f;
 }
 
 template <int P, int SB, int TB>
@@ -269,6 +304,7 @@ ChainSet make_chain_set() {
   s.layout = act_layout<P, SB, TB>;
   s.dw_setup = dw_setup<P, SB, TB>;
   s.dw_ws_bytes = dw_ws_bytes<P, SB, TB>;
+  s.fold_args = fold_args<SB, TB>;
   s.db_setup = db_setup<P, SB, TB>;
   return s;
 }

@@ -115,6 +115,13 @@ struct Net {
     return {8, tin * 32, IN_ACC, EPI_BMASK, L.w, -1, -1, mask_of(f - 1), f - 1, tin};
   }
 
+  // encoding_shape (forward layer SB + 1) has no activation, so its output Y
+  // and output gradient dA are linear in planes that ARE stored (Y of the last
+  // shape layer; dA of encoding_viewdir + the sigma-head gradient).  The weight
+  // gradients that would read them are folded through the layer instead
+  // (dw_fold_kernel), and neither plane is written: 2 KB less HBM traffic per
+  // bf16 training sample.
+  static constexpr bool stored(int p) { return p != SB + 1; }
   static constexpr int plane_width(int p) { return p == SB + TB + 3 ? 128 : 256; }
   // dA plane widths: viewdir's carries the sigma-head gradient in column 256
   static constexpr int dplane_width(int p) {

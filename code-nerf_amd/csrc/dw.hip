@@ -333,16 +333,25 @@ __global__ __launch_bounds__(256) void dw_reduce_kernel(DwRedArgs a) {
     v += a.part[slot * kPartRows * kPartCols + (size_t)n * kPartCols + c];
     if (need_db) db += a.dbpart[slot * kPartRows + n];
   }
-  if (p.map == MAP_VIEWDIR && n == p.out_real) {          // sigma-head row
-    if (c < 256) a.grads[p.w2][c] += v;
-    if (c == 0) a.grads[p.b2][0] += db;
-    return;
+  if (p.map == MAP_VIEWDIR) {
+    // columns < 256 are the last shape layer's features: Gx of the
+    // encoding_shape fold (dw_fold_kernel maps them); row out_real = sigma head
+    if (c < 256) a.fold[n * kFoldCols + c] = v;
+    if (c == 0) a.fold[n * kFoldCols + 256] = db;
+    if (n == p.out_real) {
+      if (c == 0) a.grads[p.b2][0] += db;
+      return;
+    }
+    if (c < 256) {
+      if (c == 0) a.grads[p.b][n] += db;
+      return;
+    }
   }
   if (p.z && n < p.out_real && c < p.in_real) v += db * p.z[c];
   if (n >= p.out_real) return;
   int f = c;
   if (p.map == MAP_PE) f = pe_feature(c);
-  else if (p.map == MAP_VIEWDIR && c >= 256) {
+  else if (p.map == MAP_VIEWDIR) {
     const int d = dir_feature(c - 256);
     f = d < 0 ? -1 : 256 + d;
   }
@@ -350,6 +359,68 @@ __global__ __launch_bounds__(256) void dw_reduce_kernel(DwRedArgs a) {
   if (c == 0) {
     a.grads[p.b][n] += db;
     if (p.dbout) p.dbout[n] = a.db_accum ? p.dbout[n] + db : db;
+  }
+}
+
+// ---------------------------------------------------------------- fold
+// The encoding_shape fold (chain_set.h fold_args), two small fp32 GEMMs over
+// the reduced Gx (257 x 257), one 32 x 32 output tile per workgroup:
+//   z = 0: d[W_v y-part ; w_sigma] (257 x 256)  = Gx . Wx_e^T
+//   z = 1: d[W_e | b_e]            (256 x 257)  = Wx_v^T . Gx
+// ~34 M FMAs per dW launch.
+__global__ __launch_bounds__(256) void dw_fold_kernel(DwFoldArgs a) {
+  __shared__ float As[32][33], Bs[32][33];
+  const int z = blockIdx.z;
+  const int rows = z == 0 ? kFoldRows : 256, cols = z == 0 ? 256 : kFoldCols;
+  const int i0 = blockIdx.y * 32, j0 = blockIdx.x * 32;
+  if (i0 >= rows || j0 >= cols) return;
+  const float* G = a.fold;
+  const float* We = a.params[a.w_shape];
+  const float* be = a.params[a.w_shape + 1];
+  const float* Wv = a.params[a.w_view];
+  const float* ws = a.params[a.w_sigma];
+  const int VC = a.view_cols;
+  // A(i, k) / B(k, j) of the two products; K = 257 either way
+  auto Aval = [&](int i, int k) -> float {
+    if (i >= rows || k >= 257) return 0.f;
+    if (z == 0) return G[i * kFoldCols + k];
+    return k < 256 ? Wv[k * VC + i] : ws[i];           // Wx_v[k][i]
+  };
+  auto Bval = [&](int k, int j) -> float {
+    if (k >= 257 || j >= cols) return 0.f;
+    if (z == 0) return k < 256 ? We[j * 256 + k] : be[j];   // Wx_e[j][k]
+    return G[k * kFoldCols + j];
+  };
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < 257; k0 += 32) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rr = ty + 8 * r;
+      As[rr][tx] = Aval(i0 + rr, k0 + tx);
+      Bs[rr][tx] = Bval(k0 + rr, j0 + tx);
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int k = 0; k < 32; ++k) {
+      const float b = Bs[k][tx];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r] = __builtin_fmaf(As[ty + 8 * r][k], b, acc[r]);
+    }
+    __syncthreads();
+  }
+  const int j = j0 + tx;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = i0 + ty + 8 * r;
+    if (i >= rows || j >= cols) continue;
+    if (z == 0) {
+      if (i < 256) a.grads[a.w_view][i * VC + j] += acc[r];
+      else a.grads[a.w_sigma][j] += acc[r];
+    } else {
+      if (j < 256) a.grads[a.w_shape][i * 256 + j] += acc[r];
+      else a.grads[a.w_shape + 1][i] += acc[r];
+    }
   }
 }
 

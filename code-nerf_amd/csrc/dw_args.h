@@ -93,6 +93,20 @@ struct DwRedArgs {
   // one may hold it as its second segment (gseg[p]), the others as their first
   int gfirst[kDwMaxProblems], glast[kDwMaxProblems], gseg[kDwMaxProblems];
   int db_accum;                 // dbout += (a later row range of the same step) instead of =
+  float* fold;                  // [kFoldRows][kFoldCols] Gx of the encoding_shape fold (viewdir problem)
+};
+
+// encoding_shape fold (chain_set.h fold_args): Gx = 257 rows (viewdir out
+// features + sigma head) x 257 columns (last shape layer's features + bias sum)
+constexpr int kFoldRows = 257, kFoldCols = 257;
+struct DwFoldArgs {
+  const float* fold;            // Gx, written by dw_reduce_kernel
+  const float* const* params;   // reference parameter tensors (the weights the forward used)
+  float* const* grads;          // their gradients (accumulated)
+  int w_shape;                  // encoding_shape weight index (bias = +1)
+  int w_view;                   // encoding_viewdir weight index ([256][view_cols])
+  int view_cols;                // 256 + 27
+  int w_sigma;                  // sigma head weight index (bias = +1)
 };
 
 // Bias gradients of the layers that follow a code injection only (codes-only

@@ -43,6 +43,7 @@ class Engine:
         self.pack_fwd = torch.empty(self.L.cn_packed_bytes(h, 0), dtype=torch.uint8, device=self.device)
         self.pack_bwd = torch.empty(self.L.cn_packed_bytes(h, 1), dtype=torch.uint8, device=self.device)
         self._packed_key = None
+        self._param_tab = None
         self._tables = {}
 
     def __del__(self):
@@ -100,9 +101,11 @@ class Engine:
         if key == self._packed_key:
             return
         self._check_params(params)
-        check(self.L.cn_pack_weights(self._plan, ptr(self.table(params)), ptr(self.pack_fwd),
+        tab = self.table(params)
+        check(self.L.cn_pack_weights(self._plan, ptr(tab), ptr(self.pack_fwd),
                                      ptr(self.pack_bwd) if bwd else None, self.stream), "cn_pack_weights")
         self._packed_key = key
+        self._param_tab = tab       # the weights the packs came from (mlp_dw's fold reads them)
 
     def latent_fwd(self, params, shape_code, texture_code):
         blob = torch.empty(self.blob_floats, dtype=torch.float32, device=self.device)
@@ -141,18 +144,27 @@ class Engine:
         check(fn(self._plan, ptr(self.pack_bwd), ptr(blob), M, ptr(dsigma), ptr(drgb), ptr(act), int(act_M),
                  int(row0), self.stream), "cn_mlp_bwd")
 
-    def mlp_dw(self, act, M, zvec, grads, dbuf, ws=None, act_M=0, row0=0, db_accum=False, nwg=0):
+    def mlp_dw(self, act, M, zvec, grads, dbuf, ws=None, act_M=0, row0=0, db_accum=False, nwg=0, params=None):
         """Weight gradients over rows [row0, row0 + pad(M)) (grads accumulate;
         dbuf is overwritten, or accumulated with db_accum).  ``grads``: the
         list of gradient tensors or a pointer table from ``table()``;
-        nwg: persistent workgroups (0 = one per CU)."""
+        nwg: persistent workgroups (0 = one per CU).  The encoding_shape fold
+        reads the forward's weights: ``params`` (tensors or a table), default
+        the parameters of the last ensure_packed."""
+        ptab = self._param_tab if params is None else (
+            params if isinstance(params, torch.Tensor) else self.table(params))
+        if ptab is None:
+            raise RuntimeError("mlp_dw: no packed weights (call ensure_packed before the forward)")
         if ws is None:
             ws = torch.empty(self.dw_ws_bytes(M), dtype=torch.uint8, device=self.device)
         tab = grads if isinstance(grads, torch.Tensor) else self.table(grads)
-        # the table may be used on a stream other than the one it was made on
-        tab.record_stream(torch.cuda.current_stream(self.device))
-        check(self.L.cn_mlp_dw_rows(self._plan, ptr(act), int(act_M), int(row0), M, ptr(zvec), ptr(tab), ptr(dbuf),
-                                    int(bool(db_accum)), int(nwg), ptr(ws), self.stream), "cn_mlp_dw_rows")
+        # the tables may be used on a stream other than the one they were made on
+        cur = torch.cuda.current_stream(self.device)
+        tab.record_stream(cur)
+        ptab.record_stream(cur)
+        check(self.L.cn_mlp_dw_rows(self._plan, ptr(act), int(act_M), int(row0), M, ptr(zvec),
+                                    ptr(ptab), ptr(tab), ptr(dbuf), int(bool(db_accum)), int(nwg), ptr(ws),
+                                    self.stream), "cn_mlp_dw_rows")
 
     def mlp_dbias(self, act, M, dbuf, ws=None, act_M=0):
         if ws is None:

@@ -138,7 +138,7 @@ class _CodeNeRFFunction(torch.autograd.Function):
             s, t, blob, zvec, act, *params = ctx.saved_tensors
             grads = [torch.zeros_like(p) for p in params]
             eng.mlp_bwd(blob, M, dsig, drgb, act)
-            eng.mlp_dw(act, M, zvec, grads, dbuf)
+            eng.mlp_dw(act, M, zvec, grads, dbuf, params=params)
         else:
             # recompute each part's forward into one part-sized workspace
             s, t, blob, zvec, x, v, *params = ctx.saved_tensors
@@ -151,7 +151,7 @@ class _CodeNeRFFunction(torch.autograd.Function):
                 b = min(a + P, M)
                 eng.mlp_fwd(blob, b - a, xyz=x[a:b], viewdir=v[a:b], act=act, act_M=P)
                 eng.mlp_bwd(blob, b - a, dsig[a:b], drgb[a:b], act, act_M=P)
-                eng.mlp_dw(act, b - a, zvec, gtab, dbuf, ws, act_M=P, db_accum=k > 0)
+                eng.mlp_dw(act, b - a, zvec, gtab, dbuf, ws, act_M=P, db_accum=k > 0, params=params)
         ds = torch.zeros(256, dtype=torch.float32, device=eng.device)
         dt = torch.zeros(256, dtype=torch.float32, device=eng.device)
         eng.latent_bwd(params, grads, s, t, zvec, dbuf, ds, dt)

@@ -134,9 +134,13 @@ int cn_mlp_bwd_codes(const cn_plan *plan, const void *d_pack_bwd, const float *d
 
 /* ---- weight / bias gradients, accumulated into d_grads; d_dbuf
  * (num_inject x 256) receives this call's bias gradient of every layer fed by
- * a latent code (input of cn_latent_bwd). */
+ * a latent code (input of cn_latent_bwd).  d_params: the parameter tensors the
+ * forward used (the table given to cn_pack_weights): encoding_shape's planes
+ * are not stored, its gradients and those of the layers reading its output
+ * (sigma head, encoding_viewdir) are folded through its weights. */
 int cn_mlp_dw(const cn_plan *plan, void *d_act, int M, const float *d_zvec,
-              float *const *d_grads, float *d_dbuf, void *d_ws, void *stream);
+              const float *const *d_params, float *const *d_grads, float *d_dbuf, void *d_ws,
+              void *stream);
 
 /* ---- cn_mlp_dw over rows [act_row0, act_row0 + pad(M)) of a workspace laid
  * out for act_M samples (act_row0 a multiple of 256).  db_accum != 0 adds
@@ -146,8 +150,8 @@ int cn_mlp_dw(const cn_plan *plan, void *d_act, int M, const float *d_zvec,
  * fewer leave CUs to a dX chain running beside it on another stream (at
  * least 26: a workgroup's share must not span more than two layers). */
 int cn_mlp_dw_rows(const cn_plan *plan, void *d_act, int act_M, int act_row0, int M,
-                   const float *d_zvec, float *const *d_grads, float *d_dbuf, int db_accum,
-                   int n_workgroups, void *d_ws, void *stream);
+                   const float *d_zvec, const float *const *d_params, float *const *d_grads,
+                   float *d_dbuf, int db_accum, int n_workgroups, void *d_ws, void *stream);
 
 /* ---- bias gradients of the layers after each code injection only (d_dbuf
  * [n_inject][256], as cn_mlp_dw writes them), for codes-only optimisation

@@ -94,7 +94,7 @@ def test_sample_guard_rejects_oversized_calls(fn):
     elif fn == "cn_mlp_bwd":
         rc = lib.cn_mlp_bwd(h, d, d, big, d, d, d, None)
     else:
-        rc = lib.cn_mlp_dw(h, d, big, d, d, d, d, None)
+        rc = lib.cn_mlp_dw(h, d, big, d, d, d, d, d, None)
     assert rc == -1
     assert b"CN_MAX_SAMPLES" in lib.cn_last_error()
     # a workspace laid out for more rows than the guard allows is refused too

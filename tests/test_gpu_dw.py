@@ -8,6 +8,12 @@ reference parameter set (src/model.py:11-34) as sum_m dA[m] (x) (X[m] + u) in
 float64 (u = the folded code injection, src/model.py:41-43,49-51), and checks
 the kernel's fp32 result to accumulation-order tolerance.  Both precisions;
 M ragged, so the padded tail samples are covered (their dA must be zero).
+
+encoding_shape (src/model.py:44) is linear, so its output Y_e and output
+gradient dA_e are not stored: the reference here forms them in float64 from
+the stored planes and the parameters (Y_e = W_e Y_shape + b_e,
+dA_e = W_v[:, :256]^T dA_v + w_sigma ds) -- the exact values the rounded
+planes used to approximate.
 """
 import numpy as np
 import pytest
@@ -20,10 +26,14 @@ N_PLANES = SB + TB + 4
 
 
 def plane_width(p):
+    if p == SB + 1:          # encoding_shape's output: not stored (folded, cn_layout.h Net::stored)
+        return 0
     return 128 if p == SB + TB + 3 else 256
 
 
 def dplane_width(p):
+    if p == SB + 1:
+        return 0
     return 128 if p == SB + TB + 3 else (288 if p == SB + 2 else 256)
 
 
@@ -139,12 +149,15 @@ def test_weight_gradients_match_float64_reduction(precision):
     dtype = torch.bfloat16 if precision == "bf16" else torch.float32
     es = 2 if precision == "bf16" else 4
     off = act_offsets(Mp, es)
-    Y = [decode(act, off[f"Y{p}"], plane_width(p), Mp, dtype) for p in range(N_PLANES)]
-    dA = [decode(act, off[f"dA{p}"], dplane_width(p), Mp, dtype) for p in range(N_PLANES)]
+    Y = [decode(act, off[f"Y{p}"], plane_width(p), Mp, dtype) if plane_width(p) else None for p in range(N_PLANES)]
+    dA = [decode(act, off[f"dA{p}"], dplane_width(p), Mp, dtype) if dplane_width(p) else None
+          for p in range(N_PLANES)]
+    for kind in (0, 1):      # the library reports the folded planes as absent
+        assert eng.L.cn_act_plane(eng._plan, M, kind, SB + 1, None) == -1
     d8 = decode(act, off["d8"], 32, Mp, dtype)
     pe = decode(act, off["pe"], 64, Mp, dtype)
     dr = decode(act, off["dir"], 32, Mp, dtype)
-    for a in dA + [d8]:
+    for a in [a for a in dA if a is not None] + [d8]:
         assert torch.count_nonzero(a[M:]) == 0, "padded samples must carry no gradient"
     u = zvec.double()
 
@@ -158,7 +171,6 @@ def test_weight_gradients_match_float64_reduction(precision):
     layers = [("encoding_xyz.0", dA[0], None, None)]
     for j in range(1, SB + 1):
         layers.append((f"shape_layer_{j}.0", dA[j], Y[j - 1], j - 1))
-    layers.append(("encoding_shape", dA[SB + 1], Y[SB], None))
     layers.append(("texture_layer_1.0", dA[SB + 3], Y[SB + 2], SB))
     layers.append(("rgb.0", dA[SB + TB + 3], Y[SB + TB + 2], None))
     layers.append(("rgb.2", d8[:, :3], Y[SB + TB + 3], None))
@@ -176,9 +188,15 @@ def test_weight_gradients_match_float64_reduction(precision):
     # encoding_viewdir: input [y_shape (256) | dir PE (27)]; the dA plane's
     # columns 256 + 257 carry the sigma-head gradient ds
     A5 = dA[SB + 2]
-    ref = torch.cat([A5[:, :256].T @ Y[SB + 1], scatter_cols(A5[:, :256].T @ dr, dir_slot_feature, 27)], dim=1)
+    ds = A5[:, 256] + A5[:, 257]
+    Pd = {n: p.detach().double() for n, p in zip(names, params)}
+    Ye = Y[SB] @ Pd["encoding_shape.weight"].T + Pd["encoding_shape.bias"]
+    dAe = A5[:, :256] @ Pd["encoding_viewdir.0.weight"][:, :256] + ds[:, None] * Pd["sigma.0.weight"][0][None, :]
+    dAe[M:] = 0.0
+    check("encoding_shape.weight", dAe.T @ Y[SB])
+    check("encoding_shape.bias", dAe.sum(0))
+    ref = torch.cat([A5[:, :256].T @ Ye, scatter_cols(A5[:, :256].T @ dr, dir_slot_feature, 27)], dim=1)
     check("encoding_viewdir.0.weight", ref)
     check("encoding_viewdir.0.bias", A5[:, :256].sum(0))
-    ds = A5[:, 256] + A5[:, 257]
-    check("sigma.0.weight", (ds[None, :] @ Y[SB + 1]))
+    check("sigma.0.weight", (ds[None, :] @ Ye))
     check("sigma.0.bias", ds.sum().reshape(1))

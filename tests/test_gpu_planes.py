@@ -11,7 +11,8 @@ included, and compares them with a torch emulation of the bf16 chain
 (bf16 operands, fp32 accumulation, bf16 storage):
 
   * PE plane (64 slot columns)  vs bf16(PE(x))            -- forward prologue
-  * Y planes of layers 0, 2, 4, 7 (enc_xyz, shape_2, enc_shape, rgb.0)
+  * Y planes of layers 0, 2, 5, 7 (enc_xyz, shape_2, enc_viewdir, rgb.0); the
+    encoding_shape planes (layer 4) are not stored (reported absent)
   * dA plane of rgb.0 (first backward epilogue) and of the PE layer (last)
 
 Bar: >= 99% of elements within 1 bf16 ulp (accumulation order and the
@@ -137,9 +138,12 @@ def test_bf16_planes_match_emulation(M):
     ys[6] = _bf(y)
     pre7 = lin("rgb.0", ys[6]) + P["rgb.0.bias"]
     ys[7] = _bf(torch.relu(pre7))
-    for i in (0, 2, 4, 7):
+    for i in (0, 2, 5, 7):
         off, F = plane(0, i)
         _check(f"Y{i}", _decode(act, off, F, M), ys[i])
+    for kind in (0, 1):      # encoding_shape's Y / dA: folded, never written
+        w = ctypes.c_int()
+        assert eng.L.cn_act_plane(eng._plan, M, kind, 4, ctypes.byref(w)) == -1 and w.value == 0
 
     # first backward epilogue: dA(rgb.0) = mask * (W_rgb2^T drgb)
     off, F = plane(1, 7)
