@@ -38,10 +38,15 @@ template <> struct PT<CN_P_FP32> {
   static constexpr int kBin = 144;
 };
 
+// Two floats -> packed bf16 pair (round to nearest even) in ONE
+// v_cvt_pk_bf16_f32: a vector conversion of a float2.  Built from two scalar
+// conversions (bf16x2{(__bf16)lo, (__bf16)hi}) the compiler emitted, in the
+// epilogues, one conversion per element against a zero plus a v_perm_b32
+// (3 VALU instead of 1).
 CN_DEV uint32_t pack_bf16x2(float lo, float hi) {
   typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
-  bf16x2 p = bf16x2{(__bf16)lo, (__bf16)hi};
-  return __builtin_bit_cast(uint32_t, p);
+  typedef __attribute__((ext_vector_type(2))) float f32x2;
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){lo, hi}, bf16x2));
 }
 // ReLU of two packed bf16: signed-int16 max with 0 (negative and -0 -> +0)
 CN_DEV uint32_t relu_bf16x2(uint32_t x) {
@@ -61,17 +66,16 @@ CN_DEV float relu_mask(float v, uint32_t word, int pos) {
   const uint32_t off = (uint32_t)__builtin_amdgcn_sbfe((int)word, pos, 1);
   return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, v) & ~off);
 }
-template <int PA, int PB>
+// Mask word layout (written by the forward epilogue, mask_bit below): the two
+// elements of a packed pair sit 16 bits apart, at bits 15 - q and 31 - q, so
+// ONE shift by q brings them to bits 15 and 31, and ONE v_perm_b32 (byte
+// selectors 8 / 9 replicate bits 15 / 31 of its low source) expands them into
+// the pair's 16-bit halves: 3 VALU per pair with the AND-NOT, all
+// compiler-visible.
+template <int Q>
 CN_DEV uint32_t relu_mask_bf16x2(uint32_t p, uint32_t word) {
-  // the pair mask is built in asm (two sign-extended bit extracts, halves
-  // merged by v_bfi): the compiler would rewrite a sign-extended bit into
-  // v_and + v_cmp + v_cndmask.  The final AND stays compiler-visible, so the
-  // hazard recognizer sees the VALU write that feeds the next MFMA.
-  uint32_t m2, tmp;
-  asm("v_bfe_i32 %0, %2, %3, 1\n\t"
-      "v_bfe_i32 %1, %2, %4, 1\n\t"
-      "v_bfi_b32 %0, %5, %0, %1"
-      : "=&v"(m2), "=&v"(tmp) : "v"(word), "I"(PA), "I"(PB), "s"(0xFFFFu));
+  const uint32_t w = word << Q;
+  const uint32_t m2 = __builtin_amdgcn_perm(w, w, 0x09090808u);
   return p & ~m2;
 }
 // sin and cos of v (radians) on the transcendental unit, for the bf16 path's
@@ -162,6 +166,15 @@ struct Chain {
 #define CN_CHAIN_PF 2
 #endif
   static constexpr int kPF = CN_CHAIN_PF;          // bf16 A-fragment prefetch distance (blocks)
+#ifndef CN_CHAIN_SB
+#define CN_CHAIN_SB 1
+#endif
+#ifndef CN_CHAIN_ASMLDS
+#define CN_CHAIN_ASMLDS 0
+#endif
+#ifndef CN_CHAIN_SB_MASK
+#define CN_CHAIN_SB_MASK 0x6     // VALU and SALU may cross; LDS reads, MFMAs, VMEM stay in program order
+#endif
   static constexpr int kRingBytes = NS * kChunkBytes;
   static constexpr int kBlobFloats = BiasBlob<SB, TB>::kFloats;
   static constexpr int kWsOff = BiasBlob<SB, TB>::kWs;
@@ -259,8 +272,10 @@ struct Chain {
 
     BinT bin[kBin];
     f32x16 acc[8];
+    // backward: every tile's first MFMA takes C = 0 (no zeroing VALU)
+    if constexpr (!BWD)
 #pragma unroll
-    for (int t = 0; t < 8; ++t) acc[t] = f32x16{};
+      for (int t = 0; t < 8; ++t) acc[t] = f32x16{};
 #pragma unroll
     for (int q = 0; q < kBin; ++q) bin[q] = BinT{};
 
@@ -276,15 +291,33 @@ struct Chain {
     static_for<0, D>([&](auto i) { issue<i>(a, smem, w, lane); });
 
     float sig_part = 0.f;
+#if CN_CHAIN_ASMLDS
+    const uint32_t a_base = lds_addr(smem) + lane * 16;
+#endif
     auto chunk = [&](auto cc) {
       constexpr int c = cc;
       const char* slot = smem + (c % NS) * kChunkBytes + lane * 16;
       // bf16: A fragments are read kPF blocks ahead of their MFMA (rolling
       // register buffer), so the LDS latency hides behind earlier MFMAs
       bf16x8 Abuf[kPF + 1];
+#if CN_CHAIN_ASMLDS
+      // explicit reads + counted waits: the compiler's waitcnt pass emitted
+      // lgkmcnt(0) right after the newest prefetch
+      constexpr int kLast = (c + 1) * kChunkBlocks <= S::kBlocks ? kChunkBlocks - 1 : S::kBlocks - 1 - c * kChunkBlocks;
+      auto aread = [&](auto bbc) {
+        constexpr int bb = bbc;
+        u32x4 r;
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(a_base), "n"((c % NS) * kChunkBytes + bb * kBlockBytes));
+        Abuf[bb % (kPF + 1)] = __builtin_bit_cast(bf16x8, r);
+      };
+#endif
       if constexpr (kBf16)
         static_for<0, kPF>([&](auto bb) {
+#if CN_CHAIN_ASMLDS
+          if constexpr (bb <= kLast) aread(bb);
+#else
           if constexpr (c * kChunkBlocks + bb < S::kBlocks) Abuf[bb] = *(const bf16x8*)(slot + bb * kBlockBytes);
+#endif
         });
       static_for<0, kChunkBlocks>([&](auto bb) {
         constexpr int g = c * kChunkBlocks + bb;
@@ -295,13 +328,30 @@ struct Chain {
           constexpr int kb = lb % S::bpt(li);
           const char* ap = slot + bb * kBlockBytes;
           if constexpr (kBf16) {
+#if CN_CHAIN_ASMLDS
+            if constexpr (bb + kPF <= kLast) aread(std::integral_constant<int, bb + kPF>{});
+            {
+              // reads younger than block bb's: bb + 1 .. min(bb + kPF, kLast)
+              constexpr int younger = (bb + kPF <= kLast ? bb + kPF : kLast) - bb;
+              asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(Abuf[bb % (kPF + 1)]) : "n"(younger));
+            }
+#else
             if constexpr (bb + kPF < kChunkBlocks && g + kPF < S::kBlocks)
               Abuf[(bb + kPF) % (kPF + 1)] = *(const bf16x8*)(ap + kPF * kBlockBytes);
+#endif
             acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                Abuf[bb % (kPF + 1)], __builtin_bit_cast(bf16x8, bin[kb]), acc[t], 0, 0, 0);
+                Abuf[bb % (kPF + 1)], __builtin_bit_cast(bf16x8, bin[kb]), (BWD && kb == 0) ? f32x16{} : acc[t], 0,
+                0, 0);
+#if CN_CHAIN_SB
+            // pin the (A-fragment read, MFMA) order: left alone, the machine
+            // scheduler sinks each LDS read next to its MFMA (2 buffers, a
+            // lgkmcnt(0) every other MFMA), exposing the LDS latency kPF hides
+            __builtin_amdgcn_sched_barrier(CN_CHAIN_SB_MASK);
+#endif
           } else {
             const f32x4 A = *(const f32x4*)ap;
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[0], bin[4 * kb + 0], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[0], bin[4 * kb + 0], (BWD && kb == 0) ? f32x16{} : acc[t],
+                                                          0, 0, 0);
             acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[1], bin[4 * kb + 1], acc[t], 0, 0, 0);
             acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[2], bin[4 * kb + 2], acc[t], 0, 0, 0);
             acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[3], bin[4 * kb + 3], acc[t], 0, 0, 0);
@@ -326,8 +376,10 @@ struct Chain {
     };
     static_for<0, kChunks>([&](auto kk) {
       constexpr int k = kk;
+#ifndef CN_CHAIN_NOSYNC
       wait_vmcnt<vm_wait(k)>();
       block_barrier();
+#endif   // CN_CHAIN_NOSYNC: measurement variant only (races on the ring: garbage results)
       if constexpr (k + D < kChunks) issue<k + D>(a, smem, w, lane);
       chunk(std::integral_constant<int, k>{});
     });
@@ -495,7 +547,7 @@ struct Chain {
       }
       return;
     } else {
-      uint32_t mbits[4] = {0u, 0u, 0u, 0u};
+      uint32_t mlo[4] = {0u, 0u, 0u, 0u}, mhi[4] = {0u, 0u, 0u, 0u};
       constexpr int yp = l.plane >= 0 ? l.plane : 0;
       constexpr int YF = N::plane_width(yp);
       const auto ry = slab_rsrc<E>(a.Y[yp], YF, wglob);
@@ -508,10 +560,10 @@ struct Chain {
           float v0 = acc[t][4 * g + 0], v1 = acc[t][4 * g + 1];
           float v2 = acc[t][4 * g + 2], v3 = acc[t][4 * g + 3];
           if constexpr (TRAIN && l.mask >= 0) {
-            uint32_t mb = mbits[t >> 1];
-            mb = push_sign(mb, v0); mb = push_sign(mb, v1);
-            mb = push_sign(mb, v2); mb = push_sign(mb, v3);
-            mbits[t >> 1] = mb;
+            // elements 0 / 2 into the low half, 1 / 3 into the high half
+            // (mask_bit): push order q = 8 (t & 1) + 2 g + i / 2
+            mlo[t >> 1] = push_sign(push_sign(mlo[t >> 1], v0), v2);
+            mhi[t >> 1] = push_sign(push_sign(mhi[t >> 1], v1), v3);
           }
           if constexpr (l.epi == EPI_SHAPE) {
             const f32x4 w4 = *(const f32x4*)(ws + 32 * t + 8 * g);
@@ -542,8 +594,11 @@ struct Chain {
         }
       }
       if constexpr (TRAIN && l.mask >= 0) {
+        uint32_t mw[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) mw[k] = (mhi[k] << 16) | (mlo[k] & 0xFFFFu);
         bstore128(mkrsrc(a.masks + (size_t)wglob * N::kMasks * 256), ((uint32_t)l.mask * 64 + lane) * 16,
-                  u32x4{mbits[0], mbits[1], mbits[2], mbits[3]});
+                  u32x4{mw[0], mw[1], mw[2], mw[3]});
       }
       if constexpr (l.epi == EPI_SHAPE) {
         const float tot = sig_part + __shfl_xor(sig_part, 32);
@@ -573,8 +628,11 @@ struct Chain {
   }
 
   // bit of the mask word holding the sign of element (tile t, group g, i):
-  // the forward epilogue shifts them in with v_alignbit, oldest at bit 31
-  static constexpr int mask_pos(int t, int g, int i) { return 31 - ((t & 1) * 16 + 4 * g + i); }
+  // the forward epilogue shifts elements 0 / 2 into the low half and 1 / 3
+  // into the high half with v_alignbit, oldest highest, push order
+  // q = 8 (t & 1) + 2 g + i / 2
+  static constexpr int mask_q(int t, int g, int i) { return (t & 1) * 8 + 2 * g + (i >> 1); }
+  static constexpr int mask_pos(int t, int g, int i) { return ((i & 1) ? 31 : 15) - mask_q(t, g, i); }
 
   template <int LI>
   __device__ static void epilogue_bwd(const ChainArgs& a, BinT* bin, f32x16* acc, const float* prm,
@@ -609,8 +667,8 @@ struct Chain {
             static_for<0, 2>([&](auto gi) {
               static_for<0, 4>([&](auto gg) {
                 if (gg == g && gi == (t & 1)) {
-                  p0 = relu_mask_bf16x2<mask_pos(gi, gg, 0), mask_pos(gi, gg, 1)>(p0, mw[t >> 1]);
-                  p1 = relu_mask_bf16x2<mask_pos(gi, gg, 2), mask_pos(gi, gg, 3)>(p1, mw[t >> 1]);
+                  p0 = relu_mask_bf16x2<mask_q(gi, gg, 0)>(p0, mw[t >> 1]);
+                  p1 = relu_mask_bf16x2<mask_q(gi, gg, 2)>(p1, mw[t >> 1]);
                 }
               });
             });
@@ -626,10 +684,16 @@ struct Chain {
           if constexpr (plane_of(LI)) plane_store<E>(rdA, voff, t, g, v[0], v[1], v[2], v[3]);
         }
       }
-      acc[t] = f32x16{};
     }
   }
 };
+
+#ifndef CN_CHAIN_TILEEPI
+#define CN_CHAIN_TILEEPI 0
+#endif
+}  // namespace cn
+#include "chain_tile.h"
+namespace cn {
 
 // min waves per SIMD: 8-wave workgroups -> 2 (one workgroup per CU); bf16
 // 4-wave workgroups -> 2 (two workgroups per CU, so one's prologue and
@@ -637,7 +701,11 @@ struct Chain {
 template <int P, int SB, int TB, bool BWD, int WAVES, int MODE>
 __global__ __launch_bounds__(WAVES * 64, (WAVES >= 8 ? WAVES / 4 : (P == CN_P_BF16 ? 2 : 1))) void chain_kernel(
     ChainArgs a) {
+#if CN_CHAIN_TILEEPI
+  ChainT<P, SB, TB, BWD, WAVES, MODE>::run(a);
+#else
   Chain<P, SB, TB, BWD, WAVES, MODE>::run(a);
+#endif
 }
 
 }  // namespace cn

@@ -394,11 +394,19 @@ __global__ __launch_bounds__(256) void dw_fold_kernel(DwFoldArgs a) {
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   for (int k0 = 0; k0 < 257; k0 += 32) {
+    // As[i][k], Bs[k][j]; lanes run along each operand's contiguous index
+    // (z = 0: Gx rows and W_e rows are contiguous in k; z = 1: W_v rows in i,
+    // Gx rows in j), so every global load is coalesced
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int rr = ty + 8 * r;
-      As[rr][tx] = Aval(i0 + rr, k0 + tx);
-      Bs[rr][tx] = Bval(k0 + rr, j0 + tx);
+      if (z == 0) {
+        As[rr][tx] = Aval(i0 + rr, k0 + tx);
+        Bs[tx][rr] = Bval(k0 + tx, j0 + rr);
+      } else {
+        As[tx][rr] = Aval(i0 + tx, k0 + rr);
+        Bs[rr][tx] = Bval(k0 + rr, j0 + tx);
+      }
     }
     __syncthreads();
 #pragma unroll 8
