@@ -96,20 +96,28 @@ class Timers:
         s.record()
         return s
 
-    def done(self, name, s):
+    def done(self, name, s, n=0, contended=False):
+        """n: samples the launch processed; contended: it shared the chip
+        with a launch on another stream (render.ImageStep's dX / dW overlap)."""
         if s is None:
             return
         e = torch.cuda.Event(enable_timing=True)
         e.record()
-        self.ev.setdefault(name, []).append((s, e))
+        self.ev.setdefault(name, []).append((s, e, int(n), bool(contended)))
 
     def summary(self):
         """phase -> (mean ms per launch, total ms over the timed steps)"""
         out = {}
         for k, v in self.ev.items():
-            tot = sum(s.elapsed_time(e) for s, e in v)
+            tot = sum(x[0].elapsed_time(x[1]) for x in v)
             out[k] = (tot / len(v), tot)
         return out
+
+    def split(self, name, contended):
+        """(total ms, total samples, launches) over the phase's launches that
+        did / did not share the chip"""
+        v = [x for x in self.ev.get(name, []) if x[3] == contended]
+        return sum(x[0].elapsed_time(x[1]) for x in v), sum(x[2] for x in v), len(v)
 
 
 def build_workload(args, dev, rank, world, precision, timers, dist):
@@ -319,20 +327,36 @@ def roofline(args, timers, samples_per_step, ms, overlapped):
     if args.config == "c4":
         flops.pop("dw", None)       # codes-only: the dw timer brackets the bias sums
     dom = max(flops, key=lambda k: per_step[k])
-    achieved = flops[dom] / (per_step[dom] * 1e-3) / 1e12
+    # the kernel's own roofline: its launches that ran alone (the overlapped
+    # ones share HBM and CUs with the other stream's kernel; reported apart)
+    t_alone, n_alone, l_alone = timers.split(dom, False)
+    if n_alone > 0 and t_alone > 0:
+        achieved = FLOP_PER_SAMPLE[dom] * n_alone / (t_alone * 1e-3) / 1e12
+        basis = f"{l_alone} uncontended launches of the kernel, HIP events on the launching stream"
+    else:
+        achieved = flops[dom] / (per_step[dom] * 1e-3) / 1e12
+        basis = "all launches of the kernel per step, HIP events on the launching stream"
     roof = {"bound": "mfma", "kernel": {"fwd": "chain_kernel<fwd,train>", "bwd": "chain_kernel<bwd>",
                                         "dw": "dw_kernel"}[dom],
             "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4), "traffic": load_traffic(args.config, dom),
+            "frac": round(achieved / peak, 4), "basis": basis, "traffic": load_traffic(args.config, dom),
             "ms_per_launch": {k: round(v, 4) for k, v in kern.items()},
             "launches_per_step": launches,
             "ms_per_step_by_kernel": {k: round(v, 4) for k, v in per_step.items()}}
+    if l_alone:
+        roof["ms_per_launch_uncontended"] = round(t_alone / l_alone, 4)
+    t_ov, n_ov, l_ov = timers.split(dom, True)
+    if n_ov > 0 and t_ov > 0:
+        a_ov = FLOP_PER_SAMPLE[dom] * n_ov / (t_ov * 1e-3) / 1e12
+        roof["contended"] = {"achieved": round(a_ov, 2), "frac": round(a_ov / peak, 4),
+                             "ms_per_launch": round(t_ov / l_ov, 4),
+                             "note": "launches overlapped with the other stream's kernel"}
     if overlapped and args.config != "c4":
         roof["overlap"] = ("dX chain of row range i on the main stream || dW of range i-1 on a side stream; "
                            "per-kernel spans overlap, so their sum exceeds the step")
     if "dw" in per_step and args.precision == "bf16" and args.config != "c4":
         # the weight-gradient pass streams the stored bf16 operands (dA and X
-        # planes, 8,000 B per sample at the srncar net): its HBM view
+        # planes, 6,976 B per sample at the srncar net): its HBM view
         dw_bytes = DW_BYTES_PER_SAMPLE * samples_per_step
         gbs = dw_bytes / (per_step["dw"] * 1e-3) / 1e9
         roof["dw_hbm_view"] = {"bytes_per_step": dw_bytes, "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,

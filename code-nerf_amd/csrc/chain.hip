@@ -170,6 +170,10 @@ struct Chain {
 #define CN_CHAIN_SB 1
 #endif
 #ifndef CN_CHAIN_ASMLDS
+// explicit ds_read_b128 + counted lgkmcnt waits for the A fragments.  OFF: a
+// counted lgkmcnt is only sound while no scalar load is in flight (SMEM
+// returns out of order), and the codes-only backward issues s_loads inside
+// the MFMA stream.  Measured gain when on: <= 5% (inference forward only).
 #define CN_CHAIN_ASMLDS 0
 #endif
 #ifndef CN_CHAIN_SB_MASK
@@ -690,6 +694,9 @@ struct Chain {
 
 #ifndef CN_CHAIN_TILEEPI
 #define CN_CHAIN_TILEEPI 0
+#endif
+#ifndef CN_CHAIN_2ACC
+#define CN_CHAIN_2ACC 0
 #endif
 }  // namespace cn
 #include "chain_tile.h"

@@ -118,18 +118,21 @@ struct ChainT {
       ((f32x4*)prm)[i] = ((const f32x4*)a.bias)[i];
 
     BinT bin[2][kBin];
-    f32x16 acc[2];
+    // [tile parity][k-block parity]: CN_CHAIN_2ACC splits each tile's
+    // accumulation into two independent MFMA chains (even / odd k-blocks,
+    // summed by the epilogue)
+    f32x16 acc[2][2];
 #pragma unroll
     for (int q = 0; q < kBin; ++q) bin[0][q] = bin[1][q] = BinT{};
-    acc[0] = acc[1] = f32x16{};
+    acc[0][0] = acc[1][0] = acc[0][1] = acc[1][1] = f32x16{};
 
     float ds = 0.f;
     if constexpr (!BWD) C::prologue_fwd(a, bin[0], smem, h, lane, w, m, mc, wglob, voff);
     else ds = C::prologue_bwd(a, bin[0], smem, h, lane, w, m, mc, wglob, voff);
     __syncthreads();
     if constexpr (!BWD) {
-      load_bias_tile<0>(acc[0], prm, h);
-      if constexpr (kTiles > 1) load_bias_tile<1>(acc[1], prm, h);
+      load_bias_tile<0>(acc[0][0], prm, h);
+      if constexpr (kTiles > 1) load_bias_tile<1>(acc[1][0], prm, h);
     }
 
     static_for<0, D>([&](auto i) { C::template issue<i>(a, smem, w, lane); });
@@ -155,29 +158,33 @@ struct ChainT {
           constexpr int J = tiles_before(li) + t;
           constexpr int cur = li & 1;
           const char* ap = slot + bb * kBlockBytes;
-          f32x16& ac = acc[J & 1];
+          constexpr int kp = (kBf16 && CN_CHAIN_2ACC) ? (kb & 1) : 0;
+          f32x16& ac = acc[J & 1][kp];
+          // first MFMA of a chain: C = 0 (backward; forward odd chain), else the running sum
+          constexpr bool zero_c = BWD ? kb <= kp : (kp == 1 && kb == 1);
           if constexpr (kBf16) {
             if constexpr (bb + kPF < kChunkBlocks && g + kPF < S::kBlocks)
               Abuf[(bb + kPF) % (kPF + 1)] = *(const bf16x8*)(ap + kPF * kBlockBytes);
             ac = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Abuf[bb % (kPF + 1)], __builtin_bit_cast(bf16x8, bin[cur][kb]),
-                                                         (BWD && kb == 0) ? f32x16{} : ac, 0, 0, 0);
+                                                         zero_c ? f32x16{} : ac, 0, 0, 0);
 #if CN_CHAIN_SB
             __builtin_amdgcn_sched_barrier(CN_CHAIN_SB_MASK);
 #endif
           } else {
             const f32x4 A = *(const f32x4*)ap;
-            ac = __builtin_amdgcn_mfma_f32_32x32x2f32(A[0], bin[cur][4 * kb + 0], (BWD && kb == 0) ? f32x16{} : ac, 0,
-                                                      0, 0);
+            ac = __builtin_amdgcn_mfma_f32_32x32x2f32(A[0], bin[cur][4 * kb + 0], zero_c ? f32x16{} : ac, 0, 0, 0);
             ac = __builtin_amdgcn_mfma_f32_32x32x2f32(A[1], bin[cur][4 * kb + 1], ac, 0, 0, 0);
             ac = __builtin_amdgcn_mfma_f32_32x32x2f32(A[2], bin[cur][4 * kb + 2], ac, 0, 0, 0);
             ac = __builtin_amdgcn_mfma_f32_32x32x2f32(A[3], bin[cur][4 * kb + 3], ac, 0, 0, 0);
           }
           if constexpr (kb == S::bpt(li) - 1) {
+            f32x16& a0 = acc[J & 1][0];
+            if constexpr (kBf16 && CN_CHAIN_2ACC && S::bpt(li) > 1) a0 += acc[J & 1][1];
             if constexpr (!BWD) {
-              tile_fwd<li, t>(a, bin[cur ^ 1], ac, prm, smem, h, lane, w, m, wglob, voff, sig_part, mlo, mhi);
-              if constexpr (J + 2 < kTiles) load_bias_tile<J + 2>(ac, prm, h);
+              tile_fwd<li, t>(a, bin[cur ^ 1], a0, prm, smem, h, lane, w, m, wglob, voff, sig_part, mlo, mhi);
+              if constexpr (J + 2 < kTiles) load_bias_tile<J + 2>(a0, prm, h);
             } else {
-              tile_bwd<li, t>(a, bin[cur ^ 1], ac, prm, smem, h, lane, w, m, wglob, voff, ds);
+              tile_bwd<li, t>(a, bin[cur ^ 1], a0, prm, smem, h, lane, w, m, wglob, voff, ds);
             }
           }
         }

@@ -3,8 +3,9 @@
 // The reduction runs over samples (K = M ~ 2e6): a persistent workgroup (one
 // per CU) owns the WHOLE (<= 288 x 288) gradient of one layer over one
 // byte-balanced slice of the (layer, slab) stream, so every operand byte is
-// read from HBM exactly once.  This pass is HBM-bound: 8,000 B of bf16
-// operands per sample against 0.9 MFLOP.  A 32-sample slab of a plane is one
+// read from HBM exactly once.  This pass is HBM-bound: 6,976 B of bf16
+// operands per sample (srncar net; encoding_shape folded, chain_set.h)
+// against 0.77 MFLOP.  A 32-sample slab of a plane is one
 // contiguous run (cn_layout.h); it lands in LDS unchanged and is read back
 // transposed.
 //   bf16 (DwBf16<KIND>): one compile-time body per operand shape (DwKind),
@@ -369,7 +370,10 @@ __global__ __launch_bounds__(256) void dw_reduce_kernel(DwRedArgs a) {
 //   z = 1: d[W_e | b_e]            (256 x 257)  = Wx_v^T . Gx
 // ~34 M FMAs per dW launch.
 __global__ __launch_bounds__(256) void dw_fold_kernel(DwFoldArgs a) {
-  __shared__ float As[32][33], Bs[32][33];
+  // the workgroup's whole K = 257 strips of both operands are staged at once
+  // (67 KB of LDS; one load round trip instead of one per 32-wide K step)
+  __shared__ float As[32][kFoldCols + 3];     // [i][k]
+  __shared__ float Bs[kFoldCols][33];         // [k][j]
   const int z = blockIdx.z;
   const int rows = z == 0 ? kFoldRows : 256, cols = z == 0 ? 256 : kFoldCols;
   const int i0 = blockIdx.y * 32, j0 = blockIdx.x * 32;
@@ -380,42 +384,34 @@ __global__ __launch_bounds__(256) void dw_fold_kernel(DwFoldArgs a) {
   const float* Wv = a.params[a.w_view];
   const float* ws = a.params[a.w_sigma];
   const int VC = a.view_cols;
-  // A(i, k) / B(k, j) of the two products; K = 257 either way
-  auto Aval = [&](int i, int k) -> float {
-    if (i >= rows || k >= 257) return 0.f;
-    if (z == 0) return G[i * kFoldCols + k];
-    return k < 256 ? Wv[k * VC + i] : ws[i];           // Wx_v[k][i]
-  };
-  auto Bval = [&](int k, int j) -> float {
-    if (k >= 257 || j >= cols) return 0.f;
-    if (z == 0) return k < 256 ? We[j * 256 + k] : be[j];   // Wx_e[j][k]
-    return G[k * kFoldCols + j];
-  };
+  // consecutive threads read consecutive addresses of each operand
+  if (z == 0) {
+    // A = Gx rows i0.. (contiguous), B(k, j) = [W_e | b_e][j][k]
+    for (int e = threadIdx.x; e < 32 * kFoldCols; e += 256) {
+      const int ii = e / kFoldCols, k = e - ii * kFoldCols;
+      As[ii][k] = i0 + ii < rows ? G[(size_t)(i0 + ii) * kFoldCols + k] : 0.f;
+    }
+    for (int e = threadIdx.x; e < 32 * 256; e += 256) {
+      const int jj = e >> 8, k = e & 255;
+      Bs[k][jj] = We[(size_t)(j0 + jj) * 256 + k];
+    }
+    if (threadIdx.x < 32) Bs[256][threadIdx.x] = be[j0 + threadIdx.x];
+  } else {
+    // A(i, k) = [W_v ; w_sigma][k][i] (rows of W_v contiguous in i), B = Gx
+    for (int e = threadIdx.x; e < kFoldRows * 32; e += 256) {
+      const int k = e >> 5, ii = e & 31;
+      As[ii][k] = k < 256 ? Wv[(size_t)k * VC + i0 + ii] : ws[i0 + ii];
+      Bs[k][ii] = j0 + ii < cols ? G[(size_t)k * kFoldCols + j0 + ii] : 0.f;
+    }
+  }
+  __syncthreads();
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int k0 = 0; k0 < 257; k0 += 32) {
-    // As[i][k], Bs[k][j]; lanes run along each operand's contiguous index
-    // (z = 0: Gx rows and W_e rows are contiguous in k; z = 1: W_v rows in i,
-    // Gx rows in j), so every global load is coalesced
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int rr = ty + 8 * r;
-      if (z == 0) {
-        As[rr][tx] = Aval(i0 + rr, k0 + tx);
-        Bs[tx][rr] = Bval(k0 + tx, j0 + rr);
-      } else {
-        As[tx][rr] = Aval(i0 + tx, k0 + rr);
-        Bs[rr][tx] = Bval(k0 + rr, j0 + tx);
-      }
-    }
-    __syncthreads();
 #pragma unroll 8
-    for (int k = 0; k < 32; ++k) {
-      const float b = Bs[k][tx];
+  for (int k = 0; k < kFoldCols; ++k) {
+    const float bv = Bs[k][tx];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[r] = __builtin_fmaf(As[ty + 8 * r][k], b, acc[r]);
-    }
-    __syncthreads();
+    for (int r = 0; r < 4; ++r) acc[r] = __builtin_fmaf(As[ty + 8 * r][k], bv, acc[r]);
   }
   const int j = j0 + tx;
 #pragma unroll

@@ -112,17 +112,20 @@ class ImageStep:
         cuts = [(Mp // 256) * i // k * 256 for i in range(k)] + [M]
         ranges = [(cuts[i], cuts[i + 1] - cuts[i]) for i in range(k)]
 
-        def bwd(r0, n):
+        # timers: `contended` marks launches that share the chip with a launch
+        # on the other stream (the bench reports kernel rooflines from the
+        # uncontended ones)
+        def bwd(r0, n, ov=False):
             ev = tm.mark("bwd") if tm else None
             eng.mlp_bwd(blob, n, dsig[r0:], drgb[r0:], act, act_M=cap, row0=r0)
             if tm:
-                tm.done("bwd", ev)
+                tm.done("bwd", ev, n=n, contended=ov)
 
-        def dw(r0, n, i, nwg):
+        def dw(r0, n, i, nwg, ov=False):
             ev = tm.mark("dw") if tm else None
             eng.mlp_dw(act, n, zvec, gtab, ws["dbuf"], ws["dw"], act_M=cap, row0=r0, db_accum=i > 0, nwg=nwg)
             if tm:
-                tm.done("dw", ev)
+                tm.done("dw", ev, n=n, contended=ov)
 
         if k == 1:
             bwd(0, M)
@@ -137,9 +140,9 @@ class ImageStep:
             side.wait_event(ready)
             with torch.cuda.stream(side):
                 # the last range's dW runs alone: every CU
-                dw(*ranges[i - 1], i - 1, self.dw_side_wgs if i < k else 0)
+                dw(*ranges[i - 1], i - 1, self.dw_side_wgs if i < k else 0, ov=i < k)
             if i < k:
-                bwd(*ranges[i])
+                bwd(*ranges[i], ov=True)
         main.wait_stream(side)
 
     # ------------------------------------------------------------ steps
@@ -185,7 +188,7 @@ class ImageStep:
                                  act=ws["act"], act_M=cap, act_row0=0, sigma=ws["sig"][:Mp], rgb=ws["rgb"][:Mp],
                                  codes=not weight_grads)
         if tm:
-            tm.done("fwd", ev)
+            tm.done("fwd", ev, n=M)
         dsig, drgb = ws["dsig"], ws["drgb"]
         dsig[M:Mp].zero_()
         drgb[M:Mp].zero_()
@@ -197,11 +200,11 @@ class ImageStep:
             ev = tm.mark("bwd") if tm else None
             eng.mlp_bwd(blob, M, dsig, drgb, ws["act"], codes=True, act_M=cap, row0=0)
             if tm:
-                tm.done("bwd", ev)
+                tm.done("bwd", ev, n=M)
                 ev = tm.mark("dw")
             eng.mlp_dbias(ws["act"], M, ws["dbuf"], ws["dw"], act_M=cap)
             if tm:
-                tm.done("dw", ev)
+                tm.done("dw", ev, n=M)
             grads = ws.setdefault("scratch_grads", [torch.zeros_like(p) for p in params])
         reg_out = torch.zeros(1, dtype=torch.float32, device=eng.device)
         eng.latent_bwd(params, grads, s, t, zvec, ws["dbuf"], shape_table.grad[obj_idx],
@@ -264,7 +267,7 @@ class ImageStep:
                                    z_stride=0 if z_c.dim() == 1 else Nc, n_samples=Nc, act=ws["act"], act_M=cap,
                                    act_row0=0, sigma=sig[:Mc_p], rgb=rgb[:Mc_p], codes=rc)
         if tm:
-            tm.done("fwd", ev)
+            tm.done("fwd", ev, n=Mc)
         _, loss_c, _, _ = _eng.render_loss(sig_c, rgb_c, z_c, R, Nc, gt, self.chunk, self.white_bg,
                                            dsig=dsig[:Mc], drgb=drgb[:Mc])
         if z_f is None:
@@ -276,7 +279,7 @@ class ImageStep:
                                    act=ws["act"], act_M=cap, act_row0=Mc_p, sigma=sig[Mc_p:Mp],
                                    rgb=rgb[Mc_p:Mp], codes=rc)
         if tm:
-            tm.done("fwd", ev)
+            tm.done("fwd", ev, n=Mf)
         out_f, loss_f = _eng.render_loss_fine(sig_c, rgb_c, z_c, Nc, sig_f, rgb_f, z_f, Nf, R, gt, self.chunk,
                                               dsig[:Mc], drgb[:Mc], dsig[Mc_p:Mc_p + Mf],
                                               drgb[Mc_p:Mc_p + Mf], self.white_bg)

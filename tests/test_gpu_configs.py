@@ -12,6 +12,9 @@ at their own precision and size (through the C ABI).
       relative L2 error <= 2e-2 per tensor (measured worst 6.6e-3), cosine
       >= 0.9995;
     - the AdamW update against the oracle's AdamWRef on the bf16 gradients.
+* C3 -- srnchair geometry, 8-object data-parallel batch (accumulated in one
+  process = the ranks' SUM all-reduce): bf16 summed gradients vs the HIP fp32
+  path, rgb / chunk losses of two objects vs the oracle;
 * C4 -- optimize.py: 50 views, codes only (src/optimizer.py:73-97), 64^2 x 16:
   fp32 code gradients against the oracle (rtol 2e-3 of the max), bf16 within
   relative L2 1.5e-2 of fp32 (measured 4.8e-3).
@@ -158,6 +161,76 @@ def test_c2_train_step_bf16_full_image():
     for k, v in ref_p.items():
         np.testing.assert_allclose(after16[k].cpu().numpy(), v.numpy(), rtol=1e-6, atol=1e-9, err_msg=k)
     np.testing.assert_allclose(st16.detach().cpu().numpy(), rs.numpy(), rtol=1e-6, atol=1e-9)
+
+
+# ---------------------------------------------------------------- C3
+def test_c3_srnchair_eight_objects_bf16():
+    """C3 -- srnchair geometry (near 1.25, far 2.75), 128^2, 64 + 64, bf16,
+    an 8-object data-parallel batch: 8 ranks each render one object and
+    all-reduce (SUM) their gradients (dp.GradExchange), which equals one
+    process accumulating the 8 objects' image steps (tests/test_gpu_dp.py
+    checks that equality on two ranks).  Here: the 8 accumulated bf16
+    gradients against the HIP fp32 path on the same samples (relative L2 per
+    tensor), and rgb / chunk losses of two objects against the oracle."""
+    from codenerf_amd import engine as _eng
+    from codenerf_amd.data import _object_spec, _render_object
+    from codenerf_amd.render import ImageStep
+    H, Nc, Nf, n_obj = 128, 64, 64, 8
+    R = H * H
+    near, far = 1.25, 2.75
+    params = make_params(31)
+    s0, t0 = make_codes(31, n_obj)
+    focal = 131.25
+    z = _z(near, far, Nc, 7)
+    dev = _dev()
+    scenes = []
+    for o in range(n_obj):
+        c2w = look_at_pose(2.0, -180.0 + 45.0 * o, 15.0 + 3.0 * o)
+        spec = _object_spec(np.random.Generator(np.random.PCG64(100 + o)))
+        img = _render_object(spec, c2w.astype(np.float64), H, H, focal)
+        ro, vd = _eng.get_rays_dev(H, H, focal, True, torch.tensor(c2w).to(dev))
+        scenes.append((ro, vd, torch.tensor(img.reshape(-1, 3), dtype=torch.float32).to(dev)))
+
+    def run(precision, z_fs=None):
+        m = _model(params, precision)
+        st = torch.nn.Parameter(torch.tensor(s0, device=dev))
+        tt = torch.nn.Parameter(torch.tensor(t0, device=dev))
+        step = ImageStep(m, chunk=2048, reg_coef=1e-4)
+        g = torch.Generator(device=dev).manual_seed(9)
+        out, zf_all = [], []
+        for o, (ro, vd, gt) in enumerate(scenes):
+            rand_f = torch.rand(R, Nf, device=dev, generator=g)
+            out.append(step.forward_backward_fine(ro, vd, z.to(dev), rand_f, gt, st, tt, o,
+                                                  z_f=None if z_fs is None else z_fs[o]))
+            zf_all.append(step.last_z_f.clone())
+        torch.cuda.synchronize()
+        return m, st, tt, out, zf_all
+
+    m16, st16, tt16, out16, zf = run("bf16")
+    m32, st32, tt32, _, _ = run("fp32", zf)
+    worst = []
+    for (k, p16), (_, p32) in zip(m16.named_parameters(), m32.named_parameters()):
+        e, c = _rel_l2(p16.grad, p32.grad), _cos(p16.grad, p32.grad)
+        worst.append((e, k, c))
+        assert e <= 2e-2 and c >= 0.9995, (k, e, c)
+    for a16, b32 in ((st16.grad, st32.grad), (tt16.grad, tt32.grad)):
+        assert _rel_l2(a16, b32) <= 2e-2, _rel_l2(a16, b32)
+        assert float(a16.abs().sum(1).min()) > 0.0          # every object's code row got a gradient
+    print("C3 bf16 vs fp32 summed gradient rel-L2, worst:", sorted(worst)[-3:])
+
+    st_c, tt_c = torch.tensor(s0), torch.tensor(t0)
+    p = ref_cpu.param_tensors(params, requires_grad=False)
+    for o, c in ((2, 3), (6, 5)):
+        ro, vd, gt = (t.cpu() for t in scenes[o])
+        lc, lf, rgb, _ = out16[o]
+        a, b = 2048 * c, 2048 * (c + 1)
+        with torch.no_grad():
+            lcr, lfr, rgbr = _fine_fwd(p, st_c, tt_c, o, ro[a:b], vd[a:b], z, zf[o][a:b].cpu(), gt[a:b])
+        d = (rgb[a:b].cpu() - rgbr).abs()
+        print(f"C3 object {o} chunk {c}: rgb max|d| {float(d.max()):.2e} mean {float(d.mean()):.2e}")
+        assert float(d.max()) < 1e-3 and float(d.mean()) < 2.5e-4, (o, float(d.max()), float(d.mean()))
+        np.testing.assert_allclose(float(lc[c]), lcr[0], rtol=2e-4)
+        np.testing.assert_allclose(float(lf[c]), lfr[0], rtol=2e-4)
 
 
 # ---------------------------------------------------------------- C4
