@@ -220,7 +220,7 @@ static int mlp_fwd_impl(int codes, const cn_plan* p, const void* d_pack, const f
     a.spre = (float*)(b + L.spre) + r0;
     a.masks = (uint32_t*)(b + L.masks + (r0 / 32) * L.mask_bytes_per_slab);
   }
-  const int grid = Mp / (p->cs.waves_fwd * 32);
+  const int grid = (Mp + p->cs.waves_fwd * 32 - 1) / (p->cs.waves_fwd * 32);
   hipLaunchKernelGGL(d_act ? (codes ? p->cs.fwd_codes : p->cs.fwd_train) : p->cs.fwd_infer, dim3(grid),
                      dim3(p->cs.waves_fwd * 64), 0, S(stream), a);
   return launch_check("chain_kernel(fwd)");
@@ -273,7 +273,8 @@ static int mlp_bwd_impl(int codes, const cn_plan* p, const void* d_pack, const f
   a.d8 = b + L.d8 + r0 * 32 * es;
   a.spre = (float*)(b + L.spre) + r0;
   a.masks = (uint32_t*)(b + L.masks + (r0 / 32) * L.mask_bytes_per_slab);
-  hipLaunchKernelGGL(codes ? p->cs.bwd_codes : p->cs.bwd, dim3(Mp / (p->cs.waves_bwd * 32)), dim3(p->cs.waves_bwd * 64), 0,
+  hipLaunchKernelGGL(codes ? p->cs.bwd_codes : p->cs.bwd,
+                     dim3((Mp + p->cs.waves_bwd * 32 - 1) / (p->cs.waves_bwd * 32)), dim3(p->cs.waves_bwd * 64), 0,
                      S(stream), a);
   return launch_check("chain_kernel(bwd)");
 }

@@ -116,8 +116,8 @@ CN_DEV void plane_store(__amdgpu_buffer_rsrc_t r, const uint32_t* voff, int t, i
 // descriptor, so every per-store offset stays below one slab (<= 36 KiB).  No
 // 4 GB descriptor range or 32-bit offset bounds the plane size.
 template <class E>
-CN_DEV __amdgpu_buffer_rsrc_t slab_rsrc(const void* plane, int F, int wglob) {
-  return mkrsrc((const char*)plane + (size_t)wglob * (size_t)F * 32u * sizeof(E));
+CN_DEV __amdgpu_buffer_rsrc_t slab_rsrc(const void* plane, int F, int wglob, bool live = true) {
+  return mkrsrc((const char*)plane + (size_t)wglob * (size_t)F * 32u * sizeof(E), live);
 }
 // bf16: groups 2gp and 2gp+1 of feature tile t (this lane: 4 + 4 features as
 // packed pairs) -> one 16-B store per lane.  v_permlane32_swap exchanges the
@@ -153,7 +153,10 @@ struct Chain {
   static constexpr bool PLANES = MODE == CN_MODE_TRAIN;   // every operand plane of dW
   static constexpr int NL = S::NL;
   static constexpr int kChunks = S::kChunks;
-  static constexpr int G = kChunkBlocks / WAVES;   // LDS-DMA instructions per wave per chunk
+  // waves that issue the weight stream's LDS-DMA (all of them when WAVES
+  // divides a chunk; a 12-wave workgroup lets waves 0-3 issue 4 blocks each)
+  static constexpr int kIssuers = kChunkBlocks % WAVES == 0 ? WAVES : 4;
+  static constexpr int G = kChunkBlocks / kIssuers;   // LDS-DMA instructions per issuing wave per chunk
 #ifndef CN_CHAIN_DF
 #define CN_CHAIN_DF 3
 #endif
@@ -188,7 +191,7 @@ struct Chain {
   static constexpr int kMaskOff = kDirOff + (BWD ? 0 : WAVES * 64 * kDirStash);
   static constexpr int kLdsBytes = kMaskOff + (BWD ? WAVES * N::kMasks * 1024 : 0);
   static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
-  static_assert(kChunkBlocks % WAVES == 0, "waves must divide a chunk");
+  static_assert(kChunkBlocks % kIssuers == 0, "issuing waves must divide a chunk");
   static_assert(N::kPlanes <= kMaxPlanes, "too many planes");
   static_assert(kBlobFloats % 4 == 0, "blob alignment");
 
@@ -391,6 +394,9 @@ struct Chain {
 
   template <int C>
   __device__ static void issue(const ChainArgs& a, char* smem, int w, int lane) {
+    // (non-issuing waves have no LDS-DMA to wait for: their counted vmcnt
+    // waits, sized for G DMAs per chunk, only relax towards their own stores)
+    if (kIssuers < WAVES && w >= kIssuers) return;
     const char* src = (const char*)a.wpack + (size_t)C * kChunkBytes + w * G * kBlockBytes + lane * 16;
     char* dst = smem + (C % NS) * kChunkBytes + w * G * kBlockBytes;
 #pragma unroll
@@ -494,7 +500,9 @@ struct Chain {
   }
 
   __device__ static float prologue_bwd(const ChainArgs& a, BinT* bin, char* smem, int h, int lane,
-                                       int w, int m, int mc, int wglob, const uint32_t* voff) {
+                                       int w, int m, int mc, int wglob, const uint32_t* voff, bool live = true,
+                                       int wread = -1) {
+    if (wread < 0) wread = wglob;       // slab the masks are read from (clamped for a dead wave)
     // padding samples (m >= M) get zero upstream gradients, so every dA they
     // write is exactly 0 and the dW pass can sum whole 32-sample tiles
     const bool valid = m < a.M;
@@ -516,21 +524,21 @@ struct Chain {
     if constexpr (PLANES) {
       // drgb as a padded 32-wide plane for the rgb-head weight gradient
       // (columns slot_col(0, 0..2) = 0..2)
-      const auto r8 = slab_rsrc<E>(a.d8, 32, wglob);
+      const auto r8 = slab_rsrc<E>(a.d8, 32, wglob, live);
       plane_store<E>(r8, voff, 0, 0, h ? 0.f : g0, h ? 0.f : g1, h ? 0.f : g2, 0.f);
 #pragma unroll
       for (int k = 1; k < 4; ++k) plane_store<E>(r8, voff, 0, k, 0.f, 0.f, 0.f, 0.f);
       // the sigma-head gradient rides in columns 256 (value) and 257 (its
       // rounding residual, so bf16 storage keeps ~16 significant bits) of the
       // viewdir dA plane (feature tile 8 of its 288 columns)
-      const auto rv = slab_rsrc<E>(a.dA[SB + 2], 288, wglob);
+      const auto rv = slab_rsrc<E>(a.dA[SB + 2], 288, wglob, live);
       const float ds_hi = (float)(E)ds;
       plane_store<E>(rv, voff, 8, 0, h ? 0.f : ds_hi, h ? 0.f : ds - ds_hi, 0.f, 0.f);
 #pragma unroll
       for (int k = 1; k < 4; ++k) plane_store<E>(rv, voff, 8, k, 0.f, 0.f, 0.f, 0.f);
     }
     // ReLU sign bits of this wave -> LDS
-    const u32x4* src = (const u32x4*)a.masks + (size_t)wglob * N::kMasks * 64 + lane;
+    const u32x4* src = (const u32x4*)a.masks + (size_t)wread * N::kMasks * 64 + lane;
     u32x4* dst = (u32x4*)(smem + kMaskOff) + (size_t)w * N::kMasks * 64 + lane;
 #pragma unroll
     for (int k = 0; k < N::kMasks; ++k) dst[k * 64] = src[k * 64];

@@ -107,6 +107,11 @@ struct ChainT {
     const int m = blockIdx.x * (WAVES * 32) + w * 32 + (lane & 31);
     const int mc = m < a.M ? m : a.M - 1;
     const int wglob = blockIdx.x * WAVES + w;
+    // a workgroup of WAVES * 32 samples need not divide the 256-padded rows
+    // (12-wave backward): waves past the end compute on clamped inputs and
+    // store nothing (empty buffer ranges)
+    const int nslab = ((a.M + 255) & ~255) >> 5;
+    const bool live = wglob < nslab;
     float* prm = (float*)(smem + kRingBytes);
     uint32_t voff[6];   // [g]: 8-B stores of group g; [4 + gp]: bf16 16-B pair stores
 #pragma unroll
@@ -128,7 +133,7 @@ struct ChainT {
 
     float ds = 0.f;
     if constexpr (!BWD) C::prologue_fwd(a, bin[0], smem, h, lane, w, m, mc, wglob, voff);
-    else ds = C::prologue_bwd(a, bin[0], smem, h, lane, w, m, mc, wglob, voff);
+    else ds = C::prologue_bwd(a, bin[0], smem, h, lane, w, m, mc, wglob, voff, live, live ? wglob : nslab - 1);
     __syncthreads();
     if constexpr (!BWD) {
       load_bias_tile<0>(acc[0][0], prm, h);
@@ -184,7 +189,7 @@ struct ChainT {
               tile_fwd<li, t>(a, bin[cur ^ 1], a0, prm, smem, h, lane, w, m, wglob, voff, sig_part, mlo, mhi);
               if constexpr (J + 2 < kTiles) load_bias_tile<J + 2>(a0, prm, h);
             } else {
-              tile_bwd<li, t>(a, bin[cur ^ 1], a0, prm, smem, h, lane, w, m, wglob, voff, ds);
+              tile_bwd<li, t>(a, bin[cur ^ 1], a0, prm, smem, h, lane, w, m, wglob, voff, ds, live);
             }
           }
         }
@@ -294,11 +299,11 @@ struct ChainT {
   template <int LI, int T_>
   __device__ static void tile_bwd(const ChainArgs& a, BinT* bin, const f32x16& acc, const float* prm,
                                   const char* smem, int h, int lane, int w, int m, int wglob, const uint32_t* voff,
-                                  float ds) {
+                                  float ds, bool live) {
     constexpr Layer l = S::L(LI);
     constexpr int t = T_;
     constexpr int width = N::dplane_width(l.plane);
-    const auto rdA = slab_rsrc<E>(a.dA[l.plane], width, wglob);
+    const auto rdA = slab_rsrc<E>(a.dA[l.plane], width, wglob, live);
     uint32_t mword = 0u;
     if constexpr (l.epi == EPI_BMASK)
       mword = *(const uint32_t*)(smem + kMaskOff + (((size_t)w * N::kMasks + l.mask) * 64 + lane) * 16 + 4 * (t >> 1));

@@ -99,6 +99,11 @@ template <> CN_DEV void store4<__bf16>(__bf16* p, float a, float b, float c, flo
 CN_DEV __amdgpu_buffer_rsrc_t mkrsrc(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, -1, 0x00020000);
 }
+// the same, or an empty range (every access discarded by the hardware) for a
+// wave past the end of the launch's rows
+CN_DEV __amdgpu_buffer_rsrc_t mkrsrc(const void* p, bool live) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, live ? -1 : 0, 0x00020000);
+}
 // `soff` is wave-uniform (an SGPR / inline constant), so compile-time
 // address parts never cost a VGPR.
 // Cache policy of the activation-plane stores (bits: 1 sc0, 2 nt, 16 sc1).
