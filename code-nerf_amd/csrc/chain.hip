@@ -706,6 +706,9 @@ struct Chain {
 #ifndef CN_CHAIN_2ACC
 #define CN_CHAIN_2ACC 0
 #endif
+#ifndef CN_CHAIN_DEFEPI
+#define CN_CHAIN_DEFEPI 0
+#endif
 }  // namespace cn
 #include "chain_tile.h"
 namespace cn {

@@ -49,27 +49,60 @@ struct ChainT {
     return i;
   }
 
-  // ---------------- compile-time vmcnt bookkeeping
-  // vector-memory stores a wave issues after block g (tile epilogues)
-  static constexpr int stores_at(int g) {
-    const int li = S::layer_of(g);
+  // ---------------- epilogue placement
+  // CN_CHAIN_DEFEPI: the epilogue of tile J is emitted in two halves (groups
+  // 0-1, then 2-3 + the layer finalisation) between the MFMAs of tile J + 1,
+  // after its k-blocks 1 and 3, so its VALU work issues while those MFMAs
+  // execute (left to the scheduler, the epilogue ran as one VALU burst with
+  // the matrix core idle: SQ_VALU_MFMA_COEXEC_CYCLES ~0.1 of the cycles);
+  // the last tile's epilogue follows the loop.  Otherwise the whole epilogue
+  // (half 2) follows the tile's last block.
+  static constexpr bool kDef = CN_CHAIN_DEFEPI != 0;
+  static constexpr int tile_first_block(int J) {
+    const int li = layer_of_tile(J);
+    return S::first_block(li) + (J - tiles_before(li)) * S::bpt(li);
+  }
+  static constexpr int tile_bpt(int J) { return S::bpt(layer_of_tile(J)); }
+  // global block after which part `half` of tile J's epilogue is emitted
+  // (kBlocks: after the loop)
+  static constexpr int emit_block(int J, int half) {
+    if (!kDef) return half == 2 ? tile_first_block(J) + tile_bpt(J) - 1 : -1;
+    if (half == 2) return -1;
+    if (J + 1 >= kTiles) return S::kBlocks;
+    const int b = tile_bpt(J + 1);
+    const int kb = half == 0 ? (b - 1 < 1 ? b - 1 : 1) : (b - 1 < 3 ? b - 1 : 3);
+    return tile_first_block(J + 1) + kb;
+  }
+  // vector-memory stores issued by part `half` of tile J's epilogue
+  static constexpr int stores_of_part(int J, int half) {
+    const int li = layer_of_tile(J);
     const Layer l = S::L(li);
-    const int lb = g - S::first_block(li);
-    if ((lb + 1) % S::bpt(li) != 0) return 0;
-    const int t = lb / S::bpt(li);
+    const int t = J - tiles_before(li);
     if (!BWD && l.epi == EPI_RGB) return 0;     // after the last wait: not counted (safe)
-    int s = plane_of(li) ? (kBf16 ? 2 : 4) : 0;
-    if (!BWD && t == l.T - 1) {
+    const int per_tile = plane_of(li) ? (kBf16 ? 2 : 4) : 0;
+    int s = half == 2 ? per_tile : per_tile / 2;
+    if (!BWD && half != 0 && t == l.T - 1) {
       if (TRAIN && l.mask >= 0) s += 1;
       if (l.epi == EPI_SHAPE) s += TRAIN ? 2 : 1;
     }
     return s;
   }
-  static constexpr int stores_in_chunk(int c) {
-    int s = 0;
-    for (int g = c * kChunkBlocks; g < (c + 1) * kChunkBlocks && g < S::kBlocks; ++g) s += stores_at(g);
-    return s;
+  // vector-memory stores a wave issues in each chunk (tile epilogues), built
+  // once: one walk over the tiles' epilogue parts
+  struct ChunkStores {
+    int n[kChunks + 1] = {};
+  };
+  static constexpr ChunkStores chunk_stores() {
+    ChunkStores cs{};
+    for (int J = 0; J < kTiles; ++J)
+      for (int half = 0; half < 3; ++half) {
+        const int b = emit_block(J, half);
+        if (b >= 0 && b < S::kBlocks) cs.n[b / kChunkBlocks] += stores_of_part(J, half);
+      }
+    return cs;
   }
+  static constexpr ChunkStores kChunkStores = chunk_stores();
+  static constexpr int stores_in_chunk(int c) { return c < kChunks ? kChunkStores.n[c] : 0; }
   static constexpr int issued(int i) { return i < kChunks ? C::G : 0; }
   static constexpr int vm_wait(int c) {
     int n = 0;
@@ -145,6 +178,22 @@ struct ChainT {
     float sig_part = 0.f;
     uint32_t mlo[4] = {0u, 0u, 0u, 0u}, mhi[4] = {0u, 0u, 0u, 0u};
 
+    // part `half` of global tile J's epilogue (0: groups 0-1, 1: groups 2-3 +
+    // finalisation, 2: all)
+    auto emit = [&](auto Jc, auto Hc) {
+      constexpr int J = Jc, HALF = Hc;
+      constexpr int li = layer_of_tile(J);
+      constexpr int t = J - tiles_before(li);
+      f32x16& a0 = acc[J & 1][0];
+      if constexpr (HALF != 1 && kBf16 && CN_CHAIN_2ACC && S::bpt(li) > 1) a0 += acc[J & 1][1];
+      if constexpr (!BWD) {
+        tile_fwd<li, t, HALF>(a, bin[(li & 1) ^ 1], a0, prm, smem, h, lane, w, m, wglob, voff, sig_part, mlo, mhi);
+        if constexpr (HALF != 0 && J + 2 < kTiles) load_bias_tile<J + 2>(a0, prm, h);
+      } else {
+        tile_bwd<li, t, HALF>(a, bin[(li & 1) ^ 1], a0, prm, smem, h, lane, w, m, wglob, voff, ds, live);
+      }
+    };
+
     auto chunk = [&](auto cc) {
       constexpr int c = cc;
       const char* slot = smem + (c % NS) * kChunkBytes + lane * 16;
@@ -182,15 +231,13 @@ struct ChainT {
             ac = __builtin_amdgcn_mfma_f32_32x32x2f32(A[2], bin[cur][4 * kb + 2], ac, 0, 0, 0);
             ac = __builtin_amdgcn_mfma_f32_32x32x2f32(A[3], bin[cur][4 * kb + 3], ac, 0, 0, 0);
           }
-          if constexpr (kb == S::bpt(li) - 1) {
-            f32x16& a0 = acc[J & 1][0];
-            if constexpr (kBf16 && CN_CHAIN_2ACC && S::bpt(li) > 1) a0 += acc[J & 1][1];
-            if constexpr (!BWD) {
-              tile_fwd<li, t>(a, bin[cur ^ 1], a0, prm, smem, h, lane, w, m, wglob, voff, sig_part, mlo, mhi);
-              if constexpr (J + 2 < kTiles) load_bias_tile<J + 2>(a0, prm, h);
-            } else {
-              tile_bwd<li, t>(a, bin[cur ^ 1], a0, prm, smem, h, lane, w, m, wglob, voff, ds, live);
-            }
+          if constexpr (!kDef) {
+            if constexpr (kb == S::bpt(li) - 1) emit(std::integral_constant<int, J>{}, std::integral_constant<int, 2>{});
+          } else if constexpr (J >= 1) {
+            static_for<0, 2>([&](auto hh) {
+              if constexpr (emit_block(J - 1, hh) == g)
+                emit(std::integral_constant<int, J - 1>{}, std::integral_constant<int, (int)hh>{});
+            });
           }
         }
       });
@@ -202,17 +249,23 @@ struct ChainT {
       if constexpr (k + D < kChunks) C::template issue<k + D>(a, smem, w, lane);
       chunk(std::integral_constant<int, k>{});
     });
+    if constexpr (kDef) {
+      emit(std::integral_constant<int, kTiles - 1>{}, std::integral_constant<int, 0>{});
+      emit(std::integral_constant<int, kTiles - 1>{}, std::integral_constant<int, 1>{});
+    }
   }
 
   // ---------------- forward tile epilogue: tile t of layer LI -> bin_next
-  template <int LI, int T_>
+  template <int LI, int T_, int HALF>
   __device__ static void tile_fwd(const ChainArgs& a, BinT* bin, const f32x16& acc, const float* prm, const char* smem,
                                   int h, int lane, int w, int m, int wglob, const uint32_t* voff, float& sig_part,
                                   uint32_t* mlo, uint32_t* mhi) {
     constexpr Layer l = S::L(LI);
     constexpr int t = T_;
+    constexpr int g0 = HALF == 1 ? 2 : 0, g1 = HALF == 0 ? 2 : 4;
+    constexpr bool fin = HALF != 0;
     if constexpr (l.epi == EPI_RGB) {
-      if (h == 0) {
+      if (fin && h == 0) {
         a.rgb[3 * m + 0] = acc[0];
         a.rgb[3 * m + 1] = acc[1];
         a.rgb[3 * m + 2] = acc[2];
@@ -225,7 +278,7 @@ struct ChainT {
       const float* ws = prm + kWsOff + 4 * h;
       u32x2 pg[4];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
+      for (int g = g0; g < g1; ++g) {
         float v0 = acc[4 * g + 0], v1 = acc[4 * g + 1];
         float v2 = acc[4 * g + 2], v3 = acc[4 * g + 3];
         if constexpr (TRAIN && l.mask >= 0) {
@@ -260,7 +313,7 @@ struct ChainT {
           if constexpr (plane_of(LI)) plane_store<E>(ry, voff, t, g, v0, v1, v2, v3);
         }
       }
-      if constexpr (t == l.T - 1) {
+      if constexpr (fin && t == l.T - 1) {
         if constexpr (TRAIN && l.mask >= 0) {
           uint32_t mw[4];
 #pragma unroll
@@ -296,7 +349,7 @@ struct ChainT {
   }
 
   // ---------------- backward tile epilogue: tile t of dX layer LI -> bin_next
-  template <int LI, int T_>
+  template <int LI, int T_, int HALF>
   __device__ static void tile_bwd(const ChainArgs& a, BinT* bin, const f32x16& acc, const float* prm,
                                   const char* smem, int h, int lane, int w, int m, int wglob, const uint32_t* voff,
                                   float ds, bool live) {
@@ -308,9 +361,10 @@ struct ChainT {
     if constexpr (l.epi == EPI_BMASK)
       mword = *(const uint32_t*)(smem + kMaskOff + (((size_t)w * N::kMasks + l.mask) * 64 + lane) * 16 + 4 * (t >> 1));
     const float* ws = prm + kWsOff + 4 * h;
+    constexpr int g0 = HALF == 1 ? 2 : 0, g1 = HALF == 0 ? 2 : 4;
     u32x2 pg[4];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+    for (int g = g0; g < g1; ++g) {
       float v[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {

@@ -102,7 +102,10 @@ CN_DEV __amdgpu_buffer_rsrc_t mkrsrc(const void* p) {
 // the same, or an empty range (every access discarded by the hardware) for a
 // wave past the end of the launch's rows
 CN_DEV __amdgpu_buffer_rsrc_t mkrsrc(const void* p, bool live) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, live ? -1 : 0, 0x00020000);
+  // `live` is wave-uniform; readfirstlane keeps the descriptor in SGPRs (a
+  // VGPR descriptor costs a readfirstlane waterfall loop around every store)
+  const int n = __builtin_amdgcn_readfirstlane(live ? -1 : 0);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, n, 0x00020000);
 }
 // `soff` is wave-uniform (an SGPR / inline constant), so compile-time
 // address parts never cost a VGPR.
