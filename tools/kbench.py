@@ -89,7 +89,7 @@ def main():
         t = timeit(lambda: eng.mlp_dw(buf["act"], M, zvec, grads, buf["dbuf"], buf["dw"], act_M=cap), a.reps)
         out["dw_ms"] = round(t, 4)
         out["dw_tflops"] = round(899_328 * M / t / 1e9, 1)
-        out["dw_alg_GBs"] = round(M * 250 * 1024 / 32 / t / 1e6, 1)
+        out["dw_alg_GBs"] = round(M * 6976 / t / 1e6, 1)     # operand bytes per sample (srncar net, folded)
     if "copy" in only:
         x = torch.empty(2 * 1024 ** 3, dtype=torch.uint8, device=dev)
         y = torch.empty_like(x)
