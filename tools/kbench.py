@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="fwd,bwd,dw,copy")
     ap.add_argument("--precision", default="bf16")
+    ap.add_argument("--dw-rows", default="", help="comma list of row counts: dW timed over rows [0, n) too")
     a = ap.parse_args()
     only = set(a.only.split(","))
     from codenerf_amd.model import CodeNeRF
@@ -90,6 +91,10 @@ def main():
         out["dw_ms"] = round(t, 4)
         out["dw_tflops"] = round(899_328 * M / t / 1e9, 1)
         out["dw_alg_GBs"] = round(M * 6976 / t / 1e6, 1)     # operand bytes per sample (srncar net, folded)
+        for n in [int(x) for x in a.dw_rows.split(",") if x]:
+            n = min(n, M)
+            t = timeit(lambda: eng.mlp_dw(buf["act"], n, zvec, grads, buf["dbuf"], buf["dw"], act_M=cap), a.reps)
+            out[f"dw_ms_{n}"] = round(t, 4)
     if "copy" in only:
         x = torch.empty(2 * 1024 ** 3, dtype=torch.uint8, device=dev)
         y = torch.empty_like(x)
