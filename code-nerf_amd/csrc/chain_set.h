@@ -189,8 +189,15 @@ int dw_setup(char* act, int act_M, int row0, int M, int nwg_req, const float* zv
   dw->wprefix[NP] = red->wprefix[NP] = wsum;
   red->prefix[NP] = ep;
   // a share (wsum / nwg bytes) never exceeds the smallest problem, so it
-  // holds slabs of at most two problems
-  const long long nwg = nwg_req > 0 ? std::min(nwg_req, kDwWorkgroups) : kDwWorkgroups;
+  // holds slabs of at most two problems; and it spans at least
+  // 1.5 slabs of the largest, so every workgroup between a problem's first
+  // and last holds some of its slabs (the reduction sums exactly those
+  // workgroups' partials: small M runs fewer workgroups instead of leaving
+  // empty ones in between)
+  long long max_pbytes = 0;
+  for (int k = 0; k < NP; ++k) max_pbytes = std::max<long long>(max_pbytes, dw->pbytes[k]);
+  long long nwg = nwg_req > 0 ? std::min(nwg_req, kDwWorkgroups) : kDwWorkgroups;
+  nwg = std::min(nwg, std::max(1LL, 2 * wsum / (3 * max_pbytes)));
   if ((wsum + min_total - 1) / min_total >= nwg) return -1;
   dw->nwg = red->nwg = (int)nwg;
   // which partial slots hold each problem (the kernel's own segment walk)

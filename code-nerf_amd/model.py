@@ -100,11 +100,17 @@ class _CodeNeRFFunction(torch.autograd.Function):
         if s.numel() != 256 or t.numel() != 256:
             raise ValueError("one shape and one texture code of 256 values per call (src/model.py:41-42)")
         M = x.shape[0]
+        ctx.eng, ctx.M, ctx.lead = eng, M, lead
+        ctx.code_shapes = (shape_code.shape, texture_code.shape)
+        if M == 0:
+            # empty batch (as torch's nn.Linear: empty outputs, zero gradients)
+            ctx.part = -1
+            ctx.param_shapes = [p.shape for p in params]
+            return (torch.empty(*lead, 1, dtype=torch.float32, device=dev),
+                    torch.empty(*lead, 3, dtype=torch.float32, device=dev))
         eng.ensure_packed(params, bwd=True)
         blob, zvec = eng.latent_fwd(params, s, t)
         need_grad = any(ctx.needs_input_grad[3:])
-        ctx.eng, ctx.M, ctx.lead = eng, M, lead
-        ctx.code_shapes = (shape_code.shape, texture_code.shape)
         part = eng.max_act_samples()
         if need_grad and M <= part:
             act = eng.new_act(M)
@@ -129,6 +135,9 @@ class _CodeNeRFFunction(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_sigma, g_rgb):
         eng, M = ctx.eng, ctx.M
+        if ctx.part == -1:
+            z = lambda shp: torch.zeros(shp, dtype=torch.float32, device=eng.device)
+            return (None, None, None, z(ctx.code_shapes[0]), z(ctx.code_shapes[1]), *[z(s) for s in ctx.param_shapes])
         dsig = (torch.zeros(M, device=eng.device) if g_sigma is None
                 else g_sigma.contiguous().reshape(-1).to(torch.float32))
         drgb = (torch.zeros(M, 3, device=eng.device) if g_rgb is None

@@ -113,8 +113,11 @@ def scatter_cols(dw_cols, fn, n_real):
     return out
 
 
-@pytest.mark.parametrize("precision", ["bf16", "fp32"])
-def test_weight_gradients_match_float64_reduction(precision):
+@pytest.mark.parametrize("precision,R", [("bf16", 3000 - 7), ("fp32", 3000 - 7), ("bf16", 1), ("fp32", 5),
+                                         ("bf16", 4)])
+def test_weight_gradients_match_float64_reduction(precision, R):
+    """R rays x 64 samples: ragged (191,552 samples), one ray (64 samples: one
+    partial 256-sample tile), 5 rays (320) and 4 rays (exactly one tile)."""
     from codenerf_amd.model import CodeNeRF
     dev = torch.device("cuda", 0)
     torch.manual_seed(3)
@@ -122,7 +125,7 @@ def test_weight_gradients_match_float64_reduction(precision):
     eng = m.engine()
     params = m.param_list()
     names = [n for n, _ in m.named_parameters()]
-    R, N = 3000 - 7, 64                      # ragged: M not a multiple of 256
+    N = 64
     M = R * N
     ro = torch.zeros(R, 3, device=dev) + torch.tensor([0.0, 0.4, 1.2], device=dev)
     vd = torch.nn.functional.normalize(torch.randn(R, 3, device=dev) * 0.2 + torch.tensor([0., -0.3, -1.], device=dev),

@@ -188,6 +188,23 @@ def test_module_backward_matches_oracle():
     np.testing.assert_allclose(t.grad.cpu().numpy(), tc.grad.numpy(), rtol=2e-3, atol=1e-8)
 
 
+def test_module_empty_batch():
+    """An empty batch behaves as the reference's nn.Linear stack: empty
+    outputs of the right shapes, zero gradients (no launch)."""
+    g = load("n64_16x16")
+    m = _model(g)
+    s = torch.zeros(1, 256, device=_dev(), requires_grad=True)
+    t = torch.zeros(1, 256, device=_dev(), requires_grad=True)
+    for lead in ((0,), (4, 0)):
+        xyz = torch.zeros(*lead, 3, device=_dev())
+        sig, rgb = m(xyz, xyz.clone(), s, t)
+        assert sig.shape == (*lead, 1) and rgb.shape == (*lead, 3)
+        (sig.sum() + rgb.sum()).backward()
+        for _, prm in m.named_parameters():
+            assert prm.grad is not None and float(prm.grad.abs().max()) == 0.0
+        assert float(s.grad.abs().max()) == 0.0 and float(t.grad.abs().max()) == 0.0
+
+
 def _cos(a, b):
     a, b = a.reshape(-1).double(), b.reshape(-1).double()
     return float((a @ b) / (a.norm() * b.norm() + 1e-30))
