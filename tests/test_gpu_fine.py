@@ -110,11 +110,17 @@ def _fine_step(g, precision, Nf, rnd, overlap_dw=True):
     return m, st, tt, lc, lf, rgb, step.last_z_f
 
 
-@pytest.mark.parametrize("case,Nf", [("n64_16x16", 64), ("c1_32x32_n32", 32), ("ragged_48x48_n16", 40),
-                                     ("chunks_64x64_n16", 16)])
-def test_fine_train_step_fp32_matches_oracle(case, Nf):
+@pytest.mark.parametrize("case,Nf,nrays", [("n64_16x16", 64, 0), ("c1_32x32_n32", 32, 0), ("ragged_48x48_n16", 40, 0),
+                                           ("chunks_64x64_n16", 16, 0), ("n64_16x16", 64, 1), ("c1_32x32_n32", 32, 3)])
+def test_fine_train_step_fp32_matches_oracle(case, Nf, nrays):
+    """nrays > 0: the first rays of the case only (one ray: 64 + 64 samples in
+    one partial tile, a single partial loss chunk)."""
     from oracle import ref_cpu
     g = load(case)
+    if nrays:
+        g = dict(g)
+        for k in ("rays_o", "viewdir", "gt"):
+            g[k] = g[k][:nrays]
     R = g["rays_o"].shape[0]
     rnd = torch.rand(R, Nf, generator=torch.Generator().manual_seed(5))
     m, st, tt, lc, lf, rgb, zf = _fine_step(g, "fp32", Nf, rnd)
