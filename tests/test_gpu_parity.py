@@ -188,6 +188,49 @@ def test_module_backward_matches_oracle():
     np.testing.assert_allclose(t.grad.cpu().numpy(), tc.grad.numpy(), rtol=2e-3, atol=1e-8)
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_default_net_shape_blocks_2(precision):
+    """The reference's default constructor, CodeNeRF() = 2 shape blocks
+    (src/model.py:11), through the fused image step (forward, compositing,
+    chunk MSE, dX chain, dW with the encoding_shape fold, latent backward)
+    against the oracle with the same net: fp32 at the parity bar, bf16 within
+    the bf16 operand bar."""
+    from codenerf_amd.model import CodeNeRF
+    from codenerf_amd.render import ImageStep
+    from oracle import ref_cpu
+    from oracle.params import make_codes, make_params
+    g = load("n64_16x16")
+    params = make_params(44, shape_blocks=2)
+    s0, t0 = make_codes(44, 3)
+    oi = 2
+    m = CodeNeRF(2, 1, precision=precision)
+    m.load_state_dict({k: torch.tensor(v) for k, v in params.items()})
+    m = m.to(_dev())
+    st = torch.nn.Parameter(torch.tensor(s0, device=_dev()))
+    tt = torch.nn.Parameter(torch.tensor(t0, device=_dev()))
+    ro, vd = torch.tensor(g["rays_o"]), torch.tensor(g["viewdir"])
+    z, gt = torch.tensor(g["z_vals"]), torch.tensor(g["gt"])
+    step = ImageStep(m, chunk=100, reg_coef=1e-4)
+    losses, rgb, _ = step.forward_backward(ro.to(_dev()), vd.to(_dev()), z.to(_dev()), gt.to(_dev()), st, tt, oi)
+    torch.cuda.synchronize()
+    p = ref_cpu.param_tensors(params)
+    st_r, tt_r = torch.tensor(s0, requires_grad=True), torch.tensor(t0, requires_grad=True)
+    l_r, rgb_r = ref_cpu.image_step(p, st_r, tt_r, oi, ro, vd, z, gt, chunk=100, net=dict(shape_blocks=2))
+    if precision == "fp32":
+        np.testing.assert_allclose(rgb.cpu().numpy(), rgb_r.numpy(), rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(losses.cpu().numpy(), np.array(l_r), rtol=1e-4)
+        for k, prm in m.named_parameters():
+            a, b = prm.grad.cpu().numpy(), p[k].grad.numpy()
+            np.testing.assert_allclose(a, b, rtol=2e-3, atol=2e-6 * max(1.0, np.abs(b).max()), err_msg=k)
+        for a_, b_ in ((st.grad, st_r.grad), (tt.grad, tt_r.grad)):
+            b_ = b_.numpy()
+            np.testing.assert_allclose(a_.cpu().numpy(), b_, rtol=2e-3, atol=2e-6 * max(1.0, np.abs(b_).max()))
+    else:
+        assert float((rgb.cpu() - rgb_r).abs().max()) < 3e-2
+        for k, prm in m.named_parameters():
+            assert _cos(prm.grad.cpu(), p[k].grad) > 0.99, k
+
+
 def test_module_empty_batch():
     """An empty batch behaves as the reference's nn.Linear stack: empty
     outputs of the right shapes, zero gradients (no launch)."""
