@@ -274,7 +274,8 @@ static int mlp_bwd_impl(int codes, const cn_plan* p, const void* d_pack, const f
   a.spre = (float*)(b + L.spre) + r0;
   a.masks = (uint32_t*)(b + L.masks + (r0 / 32) * L.mask_bytes_per_slab);
   hipLaunchKernelGGL(codes ? p->cs.bwd_codes : p->cs.bwd,
-                     dim3((Mp + p->cs.waves_bwd * 32 - 1) / (p->cs.waves_bwd * 32)), dim3(p->cs.waves_bwd * 64), 0,
+                     dim3((Mp + p->cs.waves_bwd * p->cs.groups_bwd * 32 - 1) / (p->cs.waves_bwd * p->cs.groups_bwd * 32)),
+                     dim3(p->cs.waves_bwd * 64), 0,
                      S(stream), a);
   return launch_check("chain_kernel(bwd)");
 }

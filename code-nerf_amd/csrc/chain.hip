@@ -709,18 +709,24 @@ struct Chain {
 #ifndef CN_CHAIN_DEFEPI
 #define CN_CHAIN_DEFEPI 0
 #endif
+#ifndef CN_CHAIN_NG2
+#define CN_CHAIN_NG2 0
+#endif
 }  // namespace cn
 #include "chain_tile.h"
+#include "chain_g2.h"
 namespace cn {
 
 // min waves per SIMD: 8-wave workgroups -> 2 (one workgroup per CU); bf16
 // 4-wave workgroups -> 2 (two workgroups per CU, so one's prologue and
 // epilogues run beside the other's MFMAs); fp32 4-wave -> 1 (512 VGPRs)
 template <int P, int SB, int TB, bool BWD, int WAVES, int MODE>
-__global__ __launch_bounds__(WAVES * 64, (WAVES >= 8 ? WAVES / 4 : (P == CN_P_BF16 ? 2 : 1))) void chain_kernel(
-    ChainArgs a) {
+__global__ __launch_bounds__(WAVES * 64, (WAVES >= 8 ? WAVES / 4
+                                                   : ((P == CN_P_BF16 && !(BWD && CN_CHAIN_NG2)) ? 2 : 1))) void
+chain_kernel(ChainArgs a) {
 #if CN_CHAIN_TILEEPI
-  ChainT<P, SB, TB, BWD, WAVES, MODE>::run(a);
+  if constexpr (BWD && CN_CHAIN_NG2 && P == CN_P_BF16) ChainG<P, SB, TB, WAVES, MODE>::run(a);
+  else ChainT<P, SB, TB, BWD, WAVES, MODE>::run(a);
 #else
   Chain<P, SB, TB, BWD, WAVES, MODE>::run(a);
 #endif

@@ -24,6 +24,7 @@ struct ActLayout {
 struct ChainSet {
   int prec = 0, SB = 0, TB = 0;
   int waves_fwd = 0, waves_bwd = 0;   // waves per workgroup of the forward / backward chain kernels
+  int groups_bwd = 1;                  // 32-sample groups per backward wave (CN_CHAIN_NG2: 2)
   int tile = 0;                        // row alignment of a launch (the 256-sample pad granule)
   int n_params = 0, n_inject = 0, n_fwd_layers = 0;
   size_t pack_fwd_bytes = 0, pack_bwd_bytes = 0;

@@ -291,6 +291,7 @@ ChainSet make_chain_set() {
   s.TB = TB;
   s.waves_fwd = WF;
   s.waves_bwd = WB;
+  s.groups_bwd = (P == CN_P_BF16 && CN_CHAIN_TILEEPI && CN_CHAIN_NG2) ? 2 : 1;
   s.tile = 256;
   s.n_params = ParamIdx{SB, TB}.count();
   s.n_inject = N::kInject;
