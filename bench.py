@@ -7,8 +7,9 @@ accumulation, synthetic SRN-cars-like data (targets ray-cast from an
 ellipsoid object by the SRN-format generator's renderer, cameras on a
 radius-1.3 sphere, focal 131.25, near/far 0.8/1.8; no dataset is available
 offline; --config c3 uses the srnchair.json geometry: near/far 1.25/2.75,
-radius 2.0).  ``train_psnr`` is the last timed step's -10 log10(mean chunk
-MSE) (src/trainer.py:99), averaged over ranks.  One step = rays -> samples -> CodeNeRF forward -> compositing +
+radius 2.0).  Train-PSNR parity (the metric's second half) is measured by
+tests/test_gpu_converge.py and tests/test_gpu_regime.py, not here: a
+random-init step's PSNR says nothing.  One step = rays -> samples -> CodeNeRF forward -> compositing +
 chunk-mean MSE (+ code regulariser) -> full backward (dX chain, dW, latent
 layers, code rows) -> [RCCL all-reduce of the gradients when N > 1] -> AdamW
 over the model and both code tables.  ``value`` = ray-samples of all ranks /
@@ -32,8 +33,17 @@ sys.path.insert(0, REPO)
 BF16_PEAK_TFLOPS = 2500.0       # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 FP32_PEAK_TFLOPS = 157.3        # fp32 MFMA
 HBM_PEAK_GBS = 8000.0
-FLOP_PER_SAMPLE = {"fwd": 899_328, "bwd": 853_248, "dw": 899_328}
-DW_BYTES_PER_SAMPLE = 6_976     # bf16 dA + X operand planes read by dw_kernel (encoding_shape folded)
+# Algorithmic FLOPs per ray-sample of each pass: the
+# forward and the dX chain as the reference's Linear layers; dW as this
+# design computes it -- the reference's 13 weight GEMMs minus encoding_shape's
+# 131,072, which dw_fold_kernel recovers per launch from the 257^2 fold
+# operand (two 257 x 257 x 257 products, DW_FOLD_FLOP per launch).
+FLOP_PER_SAMPLE = {"fwd": 899_328, "bwd": 853_248, "dw": 768_256}
+DW_FOLD_FLOP = 2 * 2 * 257 ** 3
+# Bytes per ray-sample the dW pass must read: the bf16 dA + X operand planes
+# the forward / dX chains stored (encoding_shape folded).
+DW_BYTES_PER_SAMPLE = {"bf16": 6_976, "fp32": 13_952}
+KERNEL_NAMES = {"fwd": "chain_kernel<fwd,train>", "bwd": "chain_kernel<bwd>", "dw": "dw_kernel"}
 
 
 def parse():
@@ -44,7 +54,8 @@ def parse():
     ap.add_argument("--H", type=int, default=128)
     ap.add_argument("--n-coarse", type=int, default=64)
     ap.add_argument("--n-fine", type=int, default=64)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "bf16x3", "fp32"],
+                    help="chain arithmetic: bf16 operands | bf16x3 (hi + lo operands, 3 MFMAs per block) | fp32")
     ap.add_argument("--objects", type=int, default=64)
     # other BASELINE configs, measured for DESIGN.md (the driver runs c2):
     #   c4: optimize.py test-time code optimisation, 50 views x 128^2 x 64
@@ -57,7 +68,7 @@ def parse():
     ap.add_argument("--bwd-ranges", type=int, default=None, help="row ranges of the dX / dW pipeline")
     ap.add_argument("--dw-side-wgs", type=int, default=None,
                     help="persistent workgroups of the dW launches that run beside a dX chain (0: 256)")
-    ap.add_argument("--no-fp32", action="store_true", help="skip the secondary fp32 figure of the C2 step")
+    ap.add_argument("--no-fp32", action="store_true", help="skip the secondary precisions' figures of the C2 step")
     ap.add_argument("--recompute", action="store_true",
                     help="store-vs-recompute A/B: loss forwards store masks only, a second forward writes the dW planes")
     ap.add_argument("--cpu-threads", type=int, default=None,
@@ -255,29 +266,23 @@ def main():
     value = samples_per_step * world * args.steps / dt
     ms = dt / args.steps * 1e3
 
-    # train PSNR of the last timed step (src/trainer.py:99: -10 log10 of the
-    # mean of the chunk MSEs; the fine pass's losses when n_fine > 0)
-    ls = wl["last"]["losses"]
-    ls = ls[1] if isinstance(ls, tuple) else ls
-    train_psnr = float(-10 * torch.log10(ls.float().mean()))
-    if dist is not None:
-        t = torch.tensor([train_psnr], device=dev, dtype=torch.float64)
-        dist.all_reduce(t)
-        train_psnr = float(t.item()) / world
-
     roof = roofline(args, timers, samples_per_step, ms, wl["core"].step_impl.overlap_dw)
+    H, R, radius = wl["H"], wl["R"], wl["radius"]
 
-    # the reference's own precision on the same C2 geometry (secondary figure)
-    fp32 = None
-    if args.config in ("c2", "c3") and args.precision == "bf16" and not args.no_fp32:
-        t32 = Timers()
-        wl32 = build_workload(args, dev, rank, world, "fp32", t32, dist)
-        n32 = max(5, args.steps // 5)
-        dt32, med32 = timed_run(wl32, n32, 3, t32, dist, dev)
-        fp32 = {"value": round(samples_per_step * world * n32 / dt32, 1), "unit": "ray-samples/s",
-                "ms_per_step": round(dt32 / n32 * 1e3, 3), "ms_per_step_median": round(med32, 3), "steps": n32,
-                "dtype": "fp32"}
-        del wl32
+    # the other precisions on the same C2 geometry (secondary figures): fp32
+    # is the reference's arithmetic, bf16x3 its error-compensated stand-in
+    others = {}
+    if args.config in ("c2", "c3") and not args.no_fp32:
+        del wl
+        for prec in [p for p in ("bf16", "bf16x3", "fp32") if p != args.precision]:
+            t2 = Timers()
+            wl2 = build_workload(args, dev, rank, world, prec, t2, dist)
+            n2 = max(5, args.steps // (5 if prec == "fp32" else 2))
+            dt2, med2 = timed_run(wl2, n2, 3, t2, dist, dev)
+            others[prec] = {"value": round(samples_per_step * world * n2 / dt2, 1), "unit": "ray-samples/s",
+                            "ms_per_step": round(dt2 / n2 * 1e3, 3), "ms_per_step_median": round(med2, 3),
+                            "steps": n2, "dtype": prec}
+            del wl2
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -288,23 +293,21 @@ def main():
                   "c4": "ray-samples/sec (optimize.py code optimisation step), 50 views x 128x128 x 64 samples",
                   "c3": "ray-samples/sec (train step), SRN-chairs geometry 128x128, 64 coarse + 64 fine samples",
                   "c5": "ray-samples/sec (train step), SRN-cars 256x256, 128 coarse + 128 fine samples, fp32"}
-        H = wl["H"]
         out = {
             "metric": metric[args.config],
             "value": round(value, 1), "unit": "ray-samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "ms_per_step_median": round(median, 3),
             "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
-            "data": f"synthetic ({H}x{H} ray-cast ellipsoid object per rank, poses on a radius-{wl['radius']} sphere, "
+            "data": f"synthetic ({H}x{H} ray-cast ellipsoid object per rank, poses on a radius-{radius} sphere, "
                     f"random-init weights)",
-            "train_psnr": round(train_psnr, 3),
             "config": {"workload": f"{'srnchair' if args.config == 'c3' else 'srncar'}.json net, {H}x{H} image/object/step, {args.n_coarse}+{args.n_fine} "
                                    f"samples/ray, " + ("50 views, codes-only fwd+dX+AdamW" if args.config == "c4"
                                                        else "train step incl. AdamW"),
                        "name": args.config, "objects_per_step": world,
-                       "rays_per_step_per_gpu": wl["R"], "parallelism": f"dp{world}"},
+                       "rays_per_step_per_gpu": R, "parallelism": f"dp{world}"},
             "roofline": roof,
-            "fp32": fp32,
+            "precisions": others or None,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))
@@ -312,70 +315,94 @@ def main():
         dist.destroy_process_group()
 
 
+def kernel_roofline(k, precision, timers, traffic):
+    """One kernel class against ITS bound, from its launches that ran alone
+    (HIP events on the launching stream; launches that shared the chip with
+    the other stream's kernel are reported apart under ``contended``):
+      fwd / bwd chains -- MFMA-bound: algorithmic FLOPs / time vs the dense
+        MFMA peak of the precision;
+      dw -- HBM-bound: the operand-plane bytes it must read / time vs 8 TB/s
+        (its MFMA fraction alongside)."""
+    peak_tf = FP32_PEAK_TFLOPS if precision == "fp32" else BF16_PEAK_TFLOPS
+    t, n, nl = timers.split(k, False)
+    basis = f"{nl} uncontended launches, HIP events on the launching stream"
+    if n <= 0 or t <= 0:
+        t, n, nl = timers.split(k, True)
+        basis = f"{nl} launches beside the other stream's kernel (none ran alone)"
+    if n <= 0 or t <= 0:
+        return None
+    sec = t * 1e-3
+    tf = (FLOP_PER_SAMPLE[k] * n + (DW_FOLD_FLOP * nl if k == "dw" else 0)) / sec / 1e12
+    out = {"kernel": KERNEL_NAMES[k], "ms_per_launch": round(t / nl, 4), "samples_per_launch": n // nl,
+           "basis": basis}
+    if k == "dw":
+        gbs = DW_BYTES_PER_SAMPLE["fp32" if precision == "fp32" else "bf16"] * n / sec / 1e9
+        out.update(bound="hbm", achieved=round(gbs, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                   frac=round(gbs / HBM_PEAK_GBS, 4), bytes_per_sample=DW_BYTES_PER_SAMPLE.get(
+                       "fp32" if precision == "fp32" else "bf16"),
+                   mfma={"achieved": round(tf, 2), "peak": peak_tf, "unit": "TFLOP/s",
+                         "frac": round(tf / peak_tf, 4)})
+    else:
+        out.update(bound="mfma", achieved=round(tf, 2), peak=peak_tf, unit="TFLOP/s", frac=round(tf / peak_tf, 4),
+                   flop_per_sample=FLOP_PER_SAMPLE[k])
+        if precision == "bf16x3":
+            # three bf16 MFMAs per algorithmic block: the matrix cores' own load
+            out["mfma_issued"] = {"achieved": round(3 * tf, 2), "frac": round(3 * tf / peak_tf, 4),
+                                  "note": "3 bf16 MFMAs (hi*hi, hi*lo, lo*hi) per algorithmic MFMA"}
+    out["traffic"] = traffic
+    t_ov, n_ov, l_ov = timers.split(k, True)
+    if n_ov > 0 and t_ov > 0 and "beside" not in basis:
+        out["contended"] = {"ms_per_launch": round(t_ov / l_ov, 4), "launches": l_ov,
+                            "note": "launches overlapped with the other stream's kernel"}
+    return out
+
+
 def roofline(args, timers, samples_per_step, ms, overlapped):
-    """Dominant kernel = the launch class with the most measured time per step
-    (HIP events on the stream each launch runs on); achieved = its
-    algorithmic FLOPs per step / that time."""
+    """Per-kernel rooflines (fwd and dX chains: MFMA; dW: HBM) and the
+    dominant kernel -- the class with the most measured time per step --
+    lifted to the top level (bound / achieved / peak / unit / frac / traffic)."""
     summ = timers.summary()
     if not summ:
         return None
-    kern = {k: v[0] for k, v in summ.items()}                     # ms per launch
     per_step = {k: v[1] / args.steps for k, v in summ.items()}    # ms per step (all launches)
     launches = {k: len(timers.ev[k]) / args.steps for k in timers.ev}
-    peak = BF16_PEAK_TFLOPS if args.precision == "bf16" else FP32_PEAK_TFLOPS
-    flops = {k: FLOP_PER_SAMPLE[k] * samples_per_step for k in FLOP_PER_SAMPLE if k in kern}
-    if args.config == "c4":
-        flops.pop("dw", None)       # codes-only: the dw timer brackets the bias sums
-    dom = max(flops, key=lambda k: per_step[k])
-    # the kernel's own roofline: its launches that ran alone (the overlapped
-    # ones share HBM and CUs with the other stream's kernel; reported apart)
-    t_alone, n_alone, l_alone = timers.split(dom, False)
-    if n_alone > 0 and t_alone > 0:
-        achieved = FLOP_PER_SAMPLE[dom] * n_alone / (t_alone * 1e-3) / 1e12
-        basis = f"{l_alone} uncontended launches of the kernel, HIP events on the launching stream"
-    else:
-        achieved = flops[dom] / (per_step[dom] * 1e-3) / 1e12
-        basis = "all launches of the kernel per step, HIP events on the launching stream"
-    roof = {"bound": "mfma", "kernel": {"fwd": "chain_kernel<fwd,train>", "bwd": "chain_kernel<bwd>",
-                                        "dw": "dw_kernel"}[dom],
-            "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4), "basis": basis, "traffic": load_traffic(args.config, dom),
-            "ms_per_launch": {k: round(v, 4) for k, v in kern.items()},
-            "launches_per_step": launches,
-            "ms_per_step_by_kernel": {k: round(v, 4) for k, v in per_step.items()}}
-    if l_alone:
-        roof["ms_per_launch_uncontended"] = round(t_alone / l_alone, 4)
-    t_ov, n_ov, l_ov = timers.split(dom, True)
-    if n_ov > 0 and t_ov > 0:
-        a_ov = FLOP_PER_SAMPLE[dom] * n_ov / (t_ov * 1e-3) / 1e12
-        roof["contended"] = {"achieved": round(a_ov, 2), "frac": round(a_ov / peak, 4),
-                             "ms_per_launch": round(t_ov / l_ov, 4),
-                             "note": "launches overlapped with the other stream's kernel"}
+    kinds = [k for k in FLOP_PER_SAMPLE if k in summ and not (k == "dw" and args.config == "c4")]
+    kernels = {}
+    for k in kinds:
+        r = kernel_roofline(k, args.precision, timers, load_traffic(args.config, k, args.precision))
+        if r is not None:
+            r["launches_per_step"] = launches[k]
+            r["ms_per_step"] = round(per_step[k], 4)
+            kernels[k] = r
+    if not kernels:
+        return None
+    dom = max(kernels, key=lambda k: per_step[k])
+    d = kernels[dom]
+    roof = {"bound": d["bound"], "kernel": d["kernel"], "achieved": d["achieved"], "peak": d["peak"],
+            "unit": d["unit"], "frac": d["frac"], "traffic": d["traffic"], "basis": d["basis"],
+            "ms_per_launch_uncontended": d["ms_per_launch"], "kernels": kernels}
     if overlapped and args.config != "c4":
         roof["overlap"] = ("dX chain of row range i on the main stream || dW of range i-1 on a side stream; "
                            "per-kernel spans overlap, so their sum exceeds the step")
-    if "dw" in per_step and args.precision == "bf16" and args.config != "c4":
-        # the weight-gradient pass streams the stored bf16 operands (dA and X
-        # planes, 6,976 B per sample at the srncar net): its HBM view
-        dw_bytes = DW_BYTES_PER_SAMPLE * samples_per_step
-        gbs = dw_bytes / (per_step["dw"] * 1e-3) / 1e9
-        roof["dw_hbm_view"] = {"bytes_per_step": dw_bytes, "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
-                               "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    peak = FP32_PEAK_TFLOPS if args.precision == "fp32" else BF16_PEAK_TFLOPS
     step_flops = sum(v for k, v in FLOP_PER_SAMPLE.items() if args.config != "c4" or k != "dw") * samples_per_step
     roof["step"] = {"achieved": round(step_flops / (ms * 1e-3) / 1e12, 2), "unit": "TFLOP/s",
                     "frac": round(step_flops / (ms * 1e-3) / 1e12 / peak, 4)}
     return roof
 
 
-def load_traffic(config, kernel):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3
-    PMC summary of the same config (profiles/pmc_traffic.json), or None."""
+def load_traffic(config, kernel, precision="bf16"):
+    """HBM bytes per launch of a kernel class from the committed rocprofv3
+    PMC summary of the same config and precision (profiles/pmc_traffic.json:
+    FETCH_SIZE + WRITE_SIZE passes, per launch), or None."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    key = config if precision == "bf16" else f"{config}_{precision}"
     try:
         with open(path) as f:
-            return json.load(f).get(config, {}).get(kernel)
+            t = json.load(f).get(key, {}).get(kernel)
     except OSError:
         return None
+    return None if t is None else {"hbm_bytes_per_launch": t["hbm_bytes"], "source": t["source"]}
 
 
 def cpu_model():

@@ -18,6 +18,7 @@ LIB_PATH = os.environ.get("CODENERF_LIB") or os.path.join(os.path.dirname(os.pat
 ABI_VERSION = 2
 CN_FP32 = 0
 CN_BF16 = 1
+CN_BF16X3 = 2
 
 
 class HipUnavailable(RuntimeError):

@@ -55,10 +55,13 @@ int cn_plan_create(int shape_blocks, int texture_blocks, int W, int num_xyz_freq
   *out = nullptr;
   if (W != 256 || latent_dim != 256 || num_xyz_freq != 10 || num_dir_freq != 4)
     return fail("cn_plan_create: unsupported net (need W=latent_dim=256, num_xyz_freq=10, num_dir_freq=4)");
-  if (precision != CN_FP32 && precision != CN_BF16) return fail("cn_plan_create: precision must be CN_FP32 or CN_BF16");
+  if (precision != CN_FP32 && precision != CN_BF16 && precision != CN_BF16X3)
+    return fail("cn_plan_create: precision must be CN_FP32, CN_BF16 or CN_BF16X3");
   ChainSet cs;
-  if (shape_blocks == 3 && texture_blocks == 1) cs = precision ? chain_set_bf16_3_1() : chain_set_fp32_3_1();
-  else if (shape_blocks == 2 && texture_blocks == 1) cs = precision ? chain_set_bf16_2_1() : chain_set_fp32_2_1();
+  if (shape_blocks == 3 && texture_blocks == 1)
+    cs = precision == CN_BF16X3 ? chain_set_bf16x3_3_1() : precision ? chain_set_bf16_3_1() : chain_set_fp32_3_1();
+  else if (shape_blocks == 2 && texture_blocks == 1)
+    cs = precision == CN_BF16X3 ? chain_set_bf16x3_2_1() : precision ? chain_set_bf16_2_1() : chain_set_fp32_2_1();
   else return fail("cn_plan_create: unsupported (shape_blocks, texture_blocks); built: (3,1), (2,1)");
   cn_plan* p = new cn_plan();
   p->cs = cs;
@@ -274,7 +277,7 @@ static int mlp_bwd_impl(int codes, const cn_plan* p, const void* d_pack, const f
   a.spre = (float*)(b + L.spre) + r0;
   a.masks = (uint32_t*)(b + L.masks + (r0 / 32) * L.mask_bytes_per_slab);
   hipLaunchKernelGGL(codes ? p->cs.bwd_codes : p->cs.bwd,
-                     dim3((Mp + p->cs.waves_bwd * p->cs.groups_bwd * 32 - 1) / (p->cs.waves_bwd * p->cs.groups_bwd * 32)),
+                     dim3((Mp + p->cs.waves_bwd * 32 - 1) / (p->cs.waves_bwd * 32)),
                      dim3(p->cs.waves_bwd * 64), 0,
                      S(stream), a);
   return launch_check("chain_kernel(bwd)");

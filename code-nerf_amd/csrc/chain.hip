@@ -32,6 +32,7 @@ template <> struct PT<CN_P_BF16> {
   using BinT = u32x4;            // 8 bf16 packed in 4 dwords (one MFMA B operand)
   static constexpr int kBin = 18;
 };
+template <> struct PT<CN_P_BF16X3> : PT<CN_P_BF16> {};
 template <> struct PT<CN_P_FP32> {
   using E = float;
   using BinT = float;            // one v_mfma_f32_32x32x2_f32 B operand
@@ -47,6 +48,14 @@ CN_DEV uint32_t pack_bf16x2(float lo, float hi) {
   typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
   typedef __attribute__((ext_vector_type(2))) float f32x2;
   return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){lo, hi}, bf16x2));
+}
+// bf16x3: the residual pair rn(lo - hi_lo), rn(hi - hi_hi) of a packed pair
+// p = pack_bf16x2(lo, hi) -- the operand's lo part (x - rn(x) is exact in
+// fp32, so x_hi + x_lo carries 16 significant bits)
+CN_DEV uint32_t resid_bf16x2(float lo, float hi, uint32_t p) {
+  const float rl = lo - __builtin_bit_cast(float, p << 16);
+  const float rh = hi - __builtin_bit_cast(float, p & 0xFFFF0000u);
+  return pack_bf16x2(rl, rh);
 }
 // ReLU of two packed bf16: signed-int16 max with 0 (negative and -0 -> +0)
 CN_DEV uint32_t relu_bf16x2(uint32_t x) {
@@ -148,7 +157,8 @@ struct Chain {
   using E = typename PT<P>::E;
   using BinT = typename PT<P>::BinT;
   static constexpr int kBin = PT<P>::kBin;
-  static constexpr bool kBf16 = (P == CN_P_BF16);
+  static constexpr bool kBf16 = (P != CN_P_FP32);
+  static constexpr bool kX3 = (P == CN_P_BF16X3);    // hi + lo operands, three MFMAs per block
   static constexpr bool TRAIN = MODE != CN_MODE_INFER;    // masks + sigma pre-activation
   static constexpr bool PLANES = MODE == CN_MODE_TRAIN;   // every operand plane of dW
   static constexpr int NL = S::NL;
@@ -172,13 +182,6 @@ struct Chain {
 #ifndef CN_CHAIN_SB
 #define CN_CHAIN_SB 1
 #endif
-#ifndef CN_CHAIN_ASMLDS
-// explicit ds_read_b128 + counted lgkmcnt waits for the A fragments.  OFF: a
-// counted lgkmcnt is only sound while no scalar load is in flight (SMEM
-// returns out of order), and the codes-only backward issues s_loads inside
-// the MFMA stream.  Measured gain when on: <= 5% (inference forward only).
-#define CN_CHAIN_ASMLDS 0
-#endif
 #ifndef CN_CHAIN_SB_MASK
 #define CN_CHAIN_SB_MASK 0x6     // VALU and SALU may cross; LDS reads, MFMAs, VMEM stay in program order
 #endif
@@ -186,7 +189,7 @@ struct Chain {
   static constexpr int kBlobFloats = BiasBlob<SB, TB>::kFloats;
   static constexpr int kWsOff = BiasBlob<SB, TB>::kWs;
   static constexpr int kMiscOff = BiasBlob<SB, TB>::kMisc;
-  static constexpr int kDirStash = kBf16 ? 32 : 64;      // bytes per lane
+  static constexpr int kDirStash = (kBf16 && !kX3) ? 32 : 64;      // bytes per lane (bf16x3: hi, lo)
   static constexpr int kDirOff = kRingBytes + kBlobFloats * 4;
   static constexpr int kMaskOff = kDirOff + (BWD ? 0 : WAVES * 64 * kDirStash);
   static constexpr int kLdsBytes = kMaskOff + (BWD ? WAVES * N::kMasks * 1024 : 0);
@@ -278,6 +281,7 @@ struct Chain {
       ((f32x4*)prm)[i] = ((const f32x4*)a.bias)[i];
 
     BinT bin[kBin];
+    BinT binl[kX3 ? kBin : 1];     // bf16x3: the operand's lo parts
     f32x16 acc[8];
     // backward: every tile's first MFMA takes C = 0 (no zeroing VALU)
     if constexpr (!BWD)
@@ -285,12 +289,15 @@ struct Chain {
       for (int t = 0; t < 8; ++t) acc[t] = f32x16{};
 #pragma unroll
     for (int q = 0; q < kBin; ++q) bin[q] = BinT{};
+    if constexpr (kX3)
+#pragma unroll
+      for (int q = 0; q < kBin; ++q) binl[q] = BinT{};
 
     float ds = 0.f;   // bwd: sigma-head pre-activation gradient of this sample
     if constexpr (!BWD) {
-      prologue_fwd(a, bin, smem, h, lane, w, m, mc, wglob, voff);
+      prologue_fwd(a, bin, binl, smem, h, lane, w, m, mc, wglob, voff);
     } else {
-      ds = prologue_bwd(a, bin, smem, h, lane, w, m, mc, wglob, voff);
+      ds = prologue_bwd(a, bin, binl, smem, h, lane, w, m, mc, wglob, voff);
     }
     __syncthreads();
     if constexpr (!BWD) load_bias<0>(acc, prm, h);
@@ -298,33 +305,15 @@ struct Chain {
     static_for<0, D>([&](auto i) { issue<i>(a, smem, w, lane); });
 
     float sig_part = 0.f;
-#if CN_CHAIN_ASMLDS
-    const uint32_t a_base = lds_addr(smem) + lane * 16;
-#endif
     auto chunk = [&](auto cc) {
       constexpr int c = cc;
       const char* slot = smem + (c % NS) * kChunkBytes + lane * 16;
       // bf16: A fragments are read kPF blocks ahead of their MFMA (rolling
       // register buffer), so the LDS latency hides behind earlier MFMAs
       bf16x8 Abuf[kPF + 1];
-#if CN_CHAIN_ASMLDS
-      // explicit reads + counted waits: the compiler's waitcnt pass emitted
-      // lgkmcnt(0) right after the newest prefetch
-      constexpr int kLast = (c + 1) * kChunkBlocks <= S::kBlocks ? kChunkBlocks - 1 : S::kBlocks - 1 - c * kChunkBlocks;
-      auto aread = [&](auto bbc) {
-        constexpr int bb = bbc;
-        u32x4 r;
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(a_base), "n"((c % NS) * kChunkBytes + bb * kBlockBytes));
-        Abuf[bb % (kPF + 1)] = __builtin_bit_cast(bf16x8, r);
-      };
-#endif
       if constexpr (kBf16)
         static_for<0, kPF>([&](auto bb) {
-#if CN_CHAIN_ASMLDS
-          if constexpr (bb <= kLast) aread(bb);
-#else
           if constexpr (c * kChunkBlocks + bb < S::kBlocks) Abuf[bb] = *(const bf16x8*)(slot + bb * kBlockBytes);
-#endif
         });
       static_for<0, kChunkBlocks>([&](auto bb) {
         constexpr int g = c * kChunkBlocks + bb;
@@ -332,23 +321,20 @@ struct Chain {
           constexpr int li = S::layer_of(g);
           constexpr int lb = g - S::first_block(li);
           constexpr int t = lb / S::bpt(li);
-          constexpr int kb = lb % S::bpt(li);
+          constexpr int kb = (lb % S::bpt(li)) / S::kAmul;     // MFMA k-block
+          constexpr int part = (lb % S::bpt(li)) % S::kAmul;   // bf16x3: 0 = W_hi, 1 = W_lo fragment
           const char* ap = slot + bb * kBlockBytes;
           if constexpr (kBf16) {
-#if CN_CHAIN_ASMLDS
-            if constexpr (bb + kPF <= kLast) aread(std::integral_constant<int, bb + kPF>{});
-            {
-              // reads younger than block bb's: bb + 1 .. min(bb + kPF, kLast)
-              constexpr int younger = (bb + kPF <= kLast ? bb + kPF : kLast) - bb;
-              asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(Abuf[bb % (kPF + 1)]) : "n"(younger));
-            }
-#else
             if constexpr (bb + kPF < kChunkBlocks && g + kPF < S::kBlocks)
               Abuf[(bb + kPF) % (kPF + 1)] = *(const bf16x8*)(ap + kPF * kBlockBytes);
-#endif
             acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                Abuf[bb % (kPF + 1)], __builtin_bit_cast(bf16x8, bin[kb]), (BWD && kb == 0) ? f32x16{} : acc[t], 0,
-                0, 0);
+                Abuf[bb % (kPF + 1)], __builtin_bit_cast(bf16x8, bin[kb]),
+                (BWD && kb == 0 && part == 0) ? f32x16{} : acc[t], 0, 0, 0);
+            // bf16x3: W_hi x_lo after W_hi x_hi (same A fragment); the W_lo
+            // fragment (part 1) multiplies x_hi only
+            if constexpr (kX3 && part == 0)
+              acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Abuf[bb % (kPF + 1)],
+                                                               __builtin_bit_cast(bf16x8, binl[kb]), acc[t], 0, 0, 0);
 #if CN_CHAIN_SB
             // pin the (A-fragment read, MFMA) order: left alone, the machine
             // scheduler sinks each LDS read next to its MFMA (2 buffers, a
@@ -365,9 +351,9 @@ struct Chain {
           }
           if constexpr (g == S::last_block(li)) {
             if constexpr (!BWD)
-              epilogue_fwd<li>(a, bin, acc, prm, smem, h, lane, w, m, wglob, voff, sig_part);
+              epilogue_fwd<li>(a, bin, binl, acc, prm, smem, h, lane, w, m, wglob, voff, sig_part);
             else
-              epilogue_bwd<li>(a, bin, acc, prm, smem, h, lane, w, m, wglob, voff, ds);
+              epilogue_bwd<li>(a, bin, binl, acc, prm, smem, h, lane, w, m, wglob, voff, ds);
           }
           if constexpr (deferred_at(g) >= 0) {
             constexpr int j = deferred_at(g);
@@ -383,10 +369,8 @@ struct Chain {
     };
     static_for<0, kChunks>([&](auto kk) {
       constexpr int k = kk;
-#ifndef CN_CHAIN_NOSYNC
       wait_vmcnt<vm_wait(k)>();
       block_barrier();
-#endif   // CN_CHAIN_NOSYNC: measurement variant only (races on the ring: garbage results)
       if constexpr (k + D < kChunks) issue<k + D>(a, smem, w, lane);
       chunk(std::integral_constant<int, k>{});
     });
@@ -422,7 +406,7 @@ struct Chain {
   }
 
   // ---------------- prologues
-  __device__ static void prologue_fwd(const ChainArgs& a, BinT* bin, char* smem, int h, int lane,
+  __device__ static void prologue_fwd(const ChainArgs& a, BinT* bin, BinT* binl, char* smem, int h, int lane,
                                       int w, int m, int mc, int wglob, const uint32_t* voff) {
     float x[3], d[3];
     if (a.mode == 0) {
@@ -447,7 +431,7 @@ struct Chain {
       const int comp = p % 3, oct = p / 3;
       const float v = (comp == 0 ? x[0] : comp == 1 ? x[1] : x[2]) * (float)(1 << oct);
       float sn, cs;
-      if constexpr (kBf16 && CN_PE_HW) sincos_turns(v, sn, cs);
+      if constexpr (kBf16 && !kX3 && CN_PE_HW) sincos_turns(v, sn, cs);
       else sincosf(v, &sn, &cs);
       pe[2 + 2 * k] = sn;
       pe[3 + 2 * k] = cs;
@@ -461,7 +445,7 @@ struct Chain {
       if (p >= 0) {
         const int comp = p % 3, oct = p / 3;
         const float v = (comp == 0 ? d[0] : comp == 1 ? d[1] : d[2]) * (float)(1 << oct);
-        if constexpr (kBf16 && CN_PE_HW) sincos_turns(v, sn, cs);
+        if constexpr (kBf16 && !kX3 && CN_PE_HW) sincos_turns(v, sn, cs);
         else sincosf(v, &sn, &cs);
       }
       dp[2 + 2 * k] = sn;
@@ -478,6 +462,16 @@ struct Chain {
       for (int q = 0; q < 2; ++q)
         ((u32x4*)stash)[q] = u32x4{pack_bf16x2(dp[8 * q + 0], dp[8 * q + 1]), pack_bf16x2(dp[8 * q + 2], dp[8 * q + 3]),
                                    pack_bf16x2(dp[8 * q + 4], dp[8 * q + 5]), pack_bf16x2(dp[8 * q + 6], dp[8 * q + 7])};
+      if constexpr (kX3) {
+        auto lo4 = [](const float* v, const u32x4& hi) {
+          return u32x4{resid_bf16x2(v[0], v[1], hi[0]), resid_bf16x2(v[2], v[3], hi[1]),
+                       resid_bf16x2(v[4], v[5], hi[2]), resid_bf16x2(v[6], v[7], hi[3])};
+        };
+#pragma unroll
+        for (int q = 0; q < 4; ++q) binl[q] = lo4(pe + 8 * q, bin[q]);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) ((u32x4*)stash)[2 + q] = lo4(dp + 8 * q, ((const u32x4*)stash)[q]);
+      }
     } else {
 #pragma unroll
       for (int q = 0; q < 32; ++q) bin[q] = pe[q];
@@ -499,7 +493,7 @@ struct Chain {
     }
   }
 
-  __device__ static float prologue_bwd(const ChainArgs& a, BinT* bin, char* smem, int h, int lane,
+  __device__ static float prologue_bwd(const ChainArgs& a, BinT* bin, BinT* binl, char* smem, int h, int lane,
                                        int w, int m, int mc, int wglob, const uint32_t* voff, bool live = true,
                                        int wread = -1) {
     if (wread < 0) wread = wglob;       // slab the masks are read from (clamped for a dead wave)
@@ -515,7 +509,10 @@ struct Chain {
     const float ds = valid ? a.dsigma[mc] * (s > 20.f ? 1.f : ex / (ex + 1.f)) : 0.f;
     if constexpr (kBf16) {
       // k-step 0, lane half h, element j -> drgb component 8h + j
-      if (h == 0) bin[0] = u32x4{pack_bf16x2(g0, g1), pack_bf16x2(g2, 0.f), 0u, 0u};
+      if (h == 0) {
+        bin[0] = u32x4{pack_bf16x2(g0, g1), pack_bf16x2(g2, 0.f), 0u, 0u};
+        if constexpr (kX3) binl[0] = u32x4{resid_bf16x2(g0, g1, bin[0][0]), resid_bf16x2(g2, 0.f, bin[0][1]), 0u, 0u};
+      }
     } else {
       // k-step q, lane half h -> drgb component 2q + h
       bin[0] = h ? g1 : g0;
@@ -547,7 +544,7 @@ struct Chain {
 
   // ---------------- epilogues
   template <int LI>
-  __device__ static void epilogue_fwd(const ChainArgs& a, BinT* bin, f32x16* acc, const float* prm,
+  __device__ static void epilogue_fwd(const ChainArgs& a, BinT* bin, BinT* binl, f32x16* acc, const float* prm,
                                       const char* smem, int h, int lane, int w, int m, int wglob,
                                       const uint32_t* voff, float& sig_part) {
     constexpr Layer l = S::L(LI);
@@ -585,10 +582,18 @@ struct Chain {
             sig_part = __builtin_fmaf(w4[3], v3, sig_part);
           }
           if constexpr (kBf16) {
+            if constexpr (kX3 && l.epi == EPI_RELU) {
+              v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+            }
             uint32_t p0 = pack_bf16x2(v0, v1), p1 = pack_bf16x2(v2, v3);
-            if constexpr (l.epi == EPI_RELU) { p0 = relu_bf16x2(p0); p1 = relu_bf16x2(p1); }
+            if constexpr (!kX3 && l.epi == EPI_RELU) { p0 = relu_bf16x2(p0); p1 = relu_bf16x2(p1); }
             BinT& b = bin[2 * t + (g >> 1)];
             if ((g & 1) == 0) { b[0] = p0; b[1] = p1; } else { b[2] = p0; b[3] = p1; }
+            if constexpr (kX3) {
+              const uint32_t l0 = resid_bf16x2(v0, v1, p0), l1 = resid_bf16x2(v2, v3, p1);
+              BinT& bl = binl[2 * t + (g >> 1)];
+              if ((g & 1) == 0) { bl[0] = l0; bl[1] = l1; } else { bl[2] = l0; bl[3] = l1; }
+            }
             pg[g] = u32x2{p0, p1};
             if constexpr (plane_of(LI) && !defers(LI))
               if (g & 1) plane_store_pair(ry, voff[4 + (g >> 1)], t, pg[g - 1], pg[g]);
@@ -626,6 +631,10 @@ struct Chain {
         if constexpr (kBf16) {
           bin[16] = ((const u32x4*)stash)[0];
           bin[17] = ((const u32x4*)stash)[1];
+          if constexpr (kX3) {
+            binl[16] = ((const u32x4*)stash)[2];
+            binl[17] = ((const u32x4*)stash)[3];
+          }
         } else {
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
@@ -647,7 +656,7 @@ struct Chain {
   static constexpr int mask_pos(int t, int g, int i) { return ((i & 1) ? 31 : 15) - mask_q(t, g, i); }
 
   template <int LI>
-  __device__ static void epilogue_bwd(const ChainArgs& a, BinT* bin, f32x16* acc, const float* prm,
+  __device__ static void epilogue_bwd(const ChainArgs& a, BinT* bin, BinT* binl, f32x16* acc, const float* prm,
                                       const char* smem, int h, int lane, int w, int m, int wglob,
                                       const uint32_t* voff, float ds) {
     constexpr Layer l = S::L(LI);
@@ -675,18 +684,28 @@ struct Chain {
         }
         if constexpr (kBf16) {
           uint32_t p0 = pack_bf16x2(v[0], v[1]), p1 = pack_bf16x2(v[2], v[3]);
+          uint32_t l0 = 0u, l1 = 0u;
+          if constexpr (kX3) { l0 = resid_bf16x2(v[0], v[1], p0); l1 = resid_bf16x2(v[2], v[3], p1); }
           if constexpr (l.epi == EPI_BMASK) {
             static_for<0, 2>([&](auto gi) {
               static_for<0, 4>([&](auto gg) {
                 if (gg == g && gi == (t & 1)) {
                   p0 = relu_mask_bf16x2<mask_q(gi, gg, 0)>(p0, mw[t >> 1]);
                   p1 = relu_mask_bf16x2<mask_q(gi, gg, 2)>(p1, mw[t >> 1]);
+                  if constexpr (kX3) {
+                    l0 = relu_mask_bf16x2<mask_q(gi, gg, 0)>(l0, mw[t >> 1]);
+                    l1 = relu_mask_bf16x2<mask_q(gi, gg, 2)>(l1, mw[t >> 1]);
+                  }
                 }
               });
             });
           }
           BinT& b = bin[2 * t + (g >> 1)];
           if ((g & 1) == 0) { b[0] = p0; b[1] = p1; } else { b[2] = p0; b[3] = p1; }
+          if constexpr (kX3) {
+            BinT& bl = binl[2 * t + (g >> 1)];
+            if ((g & 1) == 0) { bl[0] = l0; bl[1] = l1; } else { bl[2] = l0; bl[3] = l1; }
+          }
           pg[g] = u32x2{p0, p1};
           if constexpr (plane_of(LI) && !defers(LI))
             if (g & 1) plane_store_pair(rdA, voff[4 + (g >> 1)], t, pg[g - 1], pg[g]);
@@ -700,36 +719,14 @@ struct Chain {
   }
 };
 
-#ifndef CN_CHAIN_TILEEPI
-#define CN_CHAIN_TILEEPI 0
-#endif
-#ifndef CN_CHAIN_2ACC
-#define CN_CHAIN_2ACC 0
-#endif
-#ifndef CN_CHAIN_DEFEPI
-#define CN_CHAIN_DEFEPI 0
-#endif
-#ifndef CN_CHAIN_NG2
-#define CN_CHAIN_NG2 0
-#endif
-}  // namespace cn
-#include "chain_tile.h"
-#include "chain_g2.h"
-namespace cn {
-
 // min waves per SIMD: 8-wave workgroups -> 2 (one workgroup per CU); bf16
 // 4-wave workgroups -> 2 (two workgroups per CU, so one's prologue and
-// epilogues run beside the other's MFMAs); fp32 4-wave -> 1 (512 VGPRs)
+// epilogues run beside the other's MFMAs); fp32 and bf16x3 4-wave -> 1
+// (512 VGPRs)
 template <int P, int SB, int TB, bool BWD, int WAVES, int MODE>
-__global__ __launch_bounds__(WAVES * 64, (WAVES >= 8 ? WAVES / 4
-                                                   : ((P == CN_P_BF16 && !(BWD && CN_CHAIN_NG2)) ? 2 : 1))) void
+__global__ __launch_bounds__(WAVES * 64, (WAVES >= 8 ? WAVES / 4 : (P == CN_P_BF16 ? 2 : 1))) void
 chain_kernel(ChainArgs a) {
-#if CN_CHAIN_TILEEPI
-  if constexpr (BWD && CN_CHAIN_NG2 && P == CN_P_BF16) ChainG<P, SB, TB, WAVES, MODE>::run(a);
-  else ChainT<P, SB, TB, BWD, WAVES, MODE>::run(a);
-#else
   Chain<P, SB, TB, BWD, WAVES, MODE>::run(a);
-#endif
 }
 
 }  // namespace cn

@@ -17,19 +17,22 @@ constexpr int real_in_width(int L, int TB) {
 }
 
 inline int32_t src_idx(int tensor, int offset) { return (int32_t)(((uint32_t)tensor << 24) | (uint32_t)offset); }
+// flag of a pack-table entry: store rn(w - rn(w)) (the W_lo of bf16x3), pack_kernel
+constexpr int32_t kPackLo = 1 << 23;
 
 template <int P, int SB, int TB, bool BWD>
 std::vector<int32_t> build_pack_table() {
   using S = Sched<P, SB, TB, BWD>;
   using N = Net<SB, TB>;
-  constexpr bool bf16 = P == CN_P_BF16;
+  constexpr bool bf16 = P != CN_P_FP32;
   constexpr int EPL = S::elems_per_lane();
   std::vector<int32_t> tab((size_t)S::kChunks * kChunkBlocks * 64 * EPL, -1);
   for (int g = 0; g < S::kBlocks; ++g) {
     const int li = S::layer_of(g);
     const Layer l = S::L(li);
     const int lb = g - S::first_block(li);
-    const int t = lb / S::bpt(li), kb = lb % S::bpt(li);
+    const int t = lb / S::bpt(li), kb = (lb % S::bpt(li)) / S::kAmul;
+    const bool lo = (lb % S::bpt(li)) % S::kAmul == 1;     // bf16x3: the W_lo fragment
     for (int lane = 0; lane < 64; ++lane) {
       const int n = lane & 31, h = lane >> 5;
       const int row = 32 * t + n;
@@ -65,7 +68,7 @@ std::vector<int32_t> build_pack_table() {
           else kf = bf16 ? bf16_acc_feature(kb, h, e) : f32_acc_feature(4 * kb + e, h);
           if (kf < out_f && row < in_f) v = src_idx(l.w, kf * in_f + row);
         }
-        tab[((size_t)g * 64 + lane) * EPL + e] = v;
+        tab[((size_t)g * 64 + lane) * EPL + e] = (v >= 0 && lo) ? (v | kPackLo) : v;
       }
     }
   }
@@ -75,7 +78,7 @@ std::vector<int32_t> build_pack_table() {
 template <int P, int SB, int TB>
 ActLayout act_layout(size_t Mp) {
   using N = Net<SB, TB>;
-  const size_t es = P == CN_P_BF16 ? 2 : 4;
+  const size_t es = P != CN_P_FP32 ? 2 : 4;
   ActLayout L;
   size_t off = 0;
   auto take = [&](size_t n) { size_t o = off; off += (n + 255) & ~(size_t)255; return o; };
@@ -120,7 +123,7 @@ int dw_setup(char* act, int act_M, int row0, int M, int nwg_req, const float* zv
              DwArgs* dw, DwRedArgs* red) {
   using N = Net<SB, TB>;
   constexpr ParamIdx PI{SB, TB};
-  constexpr int ES = P == CN_P_BF16 ? 2 : 4;
+  constexpr int ES = P != CN_P_FP32 ? 2 : 4;
   const int Mp = ((M + 255) / 256) * 256;
   const int Ma = ((act_M + 255) / 256) * 256;
   if (row0 < 0 || row0 % 256 || row0 + Mp > Ma) return -1;
@@ -282,16 +285,17 @@ ChainSet make_chain_set() {
 #define CN_BWD_WAVES 8
 #endif
   // bf16: 8-wave workgroups (two waves per SIMD, one workgroup per CU) by
-  // default; fp32 (bin operand of 144 VGPRs): 4 waves, one per SIMD
+  // default; fp32 (bin operand of 144 VGPRs) and bf16x3 (hi + lo operands,
+  // 2 x 72 VGPRs, beside 128 accumulator registers): 4 waves, one per SIMD
   constexpr int WF = P == CN_P_BF16 ? CN_FWD_WAVES : 4;
   constexpr int WB = P == CN_P_BF16 ? CN_BWD_WAVES : 4;
   ChainSet s;
-  s.prec = P;
+  s.prec = P != CN_P_FP32;     // activation-plane element type: 1 = bf16 (bf16, bf16x3)
+  s.x3 = P == CN_P_BF16X3;
   s.SB = SB;
   s.TB = TB;
   s.waves_fwd = WF;
   s.waves_bwd = WB;
-  s.groups_bwd = (P == CN_P_BF16 && CN_CHAIN_TILEEPI && CN_CHAIN_NG2) ? 2 : 1;
   s.tile = 256;
   s.n_params = ParamIdx{SB, TB}.count();
   s.n_inject = N::kInject;

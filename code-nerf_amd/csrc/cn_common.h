@@ -16,7 +16,13 @@ typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
 #define CN_DEV __device__ __forceinline__
 
 // ---------------------------------------------------------------- precision
-enum { CN_P_FP32 = 0, CN_P_BF16 = 1 };
+// CN_P_BF16X3: error-compensated bf16 ("bf16x3").  The chain kernels carry
+// every weight AND every activation / upstream gradient as a bf16 hi + lo
+// pair (x_hi = rn(x), x_lo = rn(x - x_hi)) and issue three MFMAs per block
+// into one fp32 accumulator: A_hi B_hi + A_hi B_lo + A_lo B_hi (the lo x lo
+// term, ~2^-16 relative, is dropped).  Activation planes (the dW operands)
+// are stored as in CN_P_BF16.
+enum { CN_P_FP32 = 0, CN_P_BF16 = 1, CN_P_BF16X3 = 2 };
 
 // Compile-time for loop: f(std::integral_constant<int, I>) for I in [0, N).
 template <int Begin, int End, class F>

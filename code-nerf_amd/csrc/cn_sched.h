@@ -7,6 +7,7 @@
 // packed blob, so the stream is a plain linear read.
 //
 //   bf16: one block = one v_mfma_f32_32x32x16_bf16 A fragment (8 bf16 / lane)
+//   bf16x3: two blocks per k-block, the W_hi fragment then the W_lo one
 //   fp32: one block = four v_mfma_f32_32x32x2_f32 A operands (4 f32 / lane)
 #pragma once
 #include "cn_layout.h"
@@ -17,12 +18,15 @@ template <int P, int SB, int TB, bool BWD>
 struct Sched {
   using N = Net<SB, TB>;
   static constexpr int NL = BWD ? N::kBwdLayers : N::kFwdLayers;
-  static constexpr bool kBf16 = (P == 1);
+  static constexpr bool kBf16 = (P != 0);
+  // fragment blocks per MFMA k-block: bf16x3 streams W_hi and W_lo
+  // back to back (the A operand of the hi and lo MFMAs)
+  static constexpr int kAmul = (P == 2) ? 2 : 1;
   static constexpr Layer L(int i) { return BWD ? N::bwd(i) : N::fwd(i); }
   // input width in MFMA-k units: drgb input is 16 (bf16) / 8 (fp32) wide
   static constexpr int kdim(int i) { return (BWD && i == 0) ? (kBf16 ? 16 : 8) : L(i).K; }
   static constexpr int kper_block() { return kBf16 ? 16 : 8; }
-  static constexpr int bpt(int i) { return kdim(i) / kper_block(); }
+  static constexpr int bpt(int i) { return kdim(i) / kper_block() * kAmul; }
   static constexpr int lblocks(int i) { return L(i).T * bpt(i); }
   static constexpr int first_block(int i) {
     int s = 0;

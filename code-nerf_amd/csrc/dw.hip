@@ -186,9 +186,6 @@ struct DwBody {
       const char* A = smem + SL * kDwSlot;
       const char* X = A + kA * TB;
       if (!live) return;
-#ifdef CN_DW_NOCOMPUTE
-      return;     // measurement variant: the operand stream alone
-#endif
       if constexpr (!kBf16) {
         // exact fp32: K = 2 samples per MFMA; lane l reads feature l & 31 of
         // sample 2 qq + (l >> 5) (A: rows = out features, B: cols = inputs)

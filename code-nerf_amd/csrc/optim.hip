@@ -12,15 +12,20 @@
 
 namespace cn {
 
-// idx: (tensor << 24) | offset, or -1 for a zero
+// idx: (tensor << 24) | (lo << 23) | offset, or -1 for a zero; lo (bf16x3):
+// the element is w_lo = rn(w - rn(w)) instead of rn(w)
 __global__ __launch_bounds__(256) void pack_kernel(const float* const* params, const int32_t* __restrict__ idx,
                                                    int n, void* out, int bf16) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   const int e = idx[i];
-  const float v = e < 0 ? 0.f : params[(uint32_t)e >> 24][e & 0xFFFFFF];
-  if (bf16) ((__bf16*)out)[i] = (__bf16)v;
-  else ((float*)out)[i] = v;
+  const float v = e < 0 ? 0.f : params[(uint32_t)e >> 24][e & 0x7FFFFF];
+  if (bf16) {
+    const __bf16 hi = (__bf16)v;
+    ((__bf16*)out)[i] = (e >= 0 && (e & 0x800000)) ? (__bf16)(v - (float)hi) : hi;
+  } else {
+    ((float*)out)[i] = v;
+  }
 }
 
 constexpr int kAdamMaxSeg = 48;

@@ -6,8 +6,9 @@ exchange
 
   * the model gradients: one SUM all-reduce of a flat fp32 bucket (714,756
     floats = 2.86 MB at the srncar net; RCCL over xGMI on MI355X, gloo in the
-    CPU tests), issued asynchronously so the code-table exchange and the
-    code-table AdamW run while it is in flight;
+    CPU tests), issued asynchronously AFTER the small code-row exchange below
+    (on one communicator, a collective queued behind it would wait for it),
+    so the code tables' AdamW runs while it is in flight;
   * the code-table gradients, which are row-sparse (a rank touches only the
     rows of the objects it rendered): an all_gather of (row index, shape row,
     texture row) = 513 floats per rendered object, scattered back into the
@@ -84,30 +85,43 @@ class GradExchange:
         if handle is not None:
             handle.wait()
 
-    def exchange_rows(self, rows):
+    def exchange_rows(self, rows, max_rows=None):
         """All-gather the gradient rows ``rows`` (object indices this rank
-        rendered, the same count on every rank) of every code table and
-        rebuild the dense gradient tables from them, identically on every
-        rank.  Payload per object: 1 + 256 x n_tables floats."""
+        rendered; duplicates are taken once) of every code table and rebuild
+        the dense gradient tables from them, identically on every rank.
+        Payload per object: 1 + 256 x n_tables floats.  Ranks may pass
+        different counts: every rank pads to ``max_rows`` (default: the
+        largest count, agreed by one small all_gather first) with index -1
+        rows, which are dropped."""
         if not self.active:
             return
         dist, group = self.dist, self.group
         world = dist.get_world_size(group)
         t0 = self.tables[0]
         dev = torch.device("cpu") if dist.get_backend(group) == "gloo" else t0.device
-        idx = torch.as_tensor(list(rows), dtype=torch.long, device=t0.device)
-        k = idx.numel()
+        uniq = sorted(set(int(r) for r in rows))
+        k = len(uniq)
+        if max_rows is None:
+            cnt = torch.tensor([k], dtype=torch.int64, device=dev)
+            cnts = [torch.empty_like(cnt) for _ in range(world)]
+            dist.all_gather(cnts, cnt, group=group)
+            max_rows = int(max(int(c) for c in cnts))
+        if k > max_rows:
+            raise ValueError(f"exchange_rows: {k} rows exceed max_rows={max_rows}")
+        idx = torch.as_tensor(uniq, dtype=torch.long, device=t0.device)
         width = sum(t.shape[1] for t in self.tables)
-        mine = torch.empty(k, 1 + width, dtype=torch.float32, device=t0.device)
-        mine[:, 0] = idx.to(torch.float32)              # exact: object counts are far below 2^24
+        mine = torch.zeros(max_rows, 1 + width, dtype=torch.float32, device=t0.device)
+        mine[:, 0] = -1.0
+        mine[:k, 0] = idx.to(torch.float32)             # exact: object counts are far below 2^24
         off = 1
         for t in self.tables:
-            mine[:, off:off + t.shape[1]] = t.grad[idx]
+            mine[:k, off:off + t.shape[1]] = t.grad[idx]
             off += t.shape[1]
         mine = mine.to(dev)
         got = [torch.empty_like(mine) for _ in range(world)]
         dist.all_gather(got, mine, group=group)
         allrows = torch.cat(got).to(t0.device)          # rank order: identical on every rank
+        allrows = allrows[allrows[:, 0] >= 0]
         rid = allrows[:, 0].long()
         off = 1
         for t in self.tables:

@@ -116,8 +116,8 @@ class Trainer:
                 else:
                     loss_per_img, rgb, reg = self.step_impl.forward_backward(
                         rays_o, viewdir, z, gt, self.shape_codes.weight, self.texture_codes.weight, oi)
-            work = self.exchange.start_model()           # data parallel: async model all-reduce
-            self.exchange.exchange_rows([oi])            # + the touched code rows
+            self.exchange.exchange_rows([oi], 1)          # data parallel: the touched code rows,
+            work = self.exchange.start_model()           # then the async model all-reduce
             self.opts.step(groups=[1, 2])
             self.exchange.finish(work)
             self.opts.step(groups=[0])

@@ -63,11 +63,14 @@ class TrainCore:
         return losses, rgb
 
     def step_grads(self, rows):
-        """Exchange (data parallel) and apply the gradients: the model bucket's
-        all-reduce runs while the touched code rows are all-gathered and the
-        code tables take their AdamW step; then the model's AdamW step."""
+        """Exchange (data parallel) and apply the gradients: the touched code
+        rows are all-gathered first (a few KB: issued behind the 2.86 MB
+        model all-reduce on the same communicator it would wait for it), then
+        the model bucket's all-reduce is issued asynchronously and the code
+        tables take their AdamW step while it is in flight; then the model's
+        AdamW step."""
+        self.exchange.exchange_rows(rows, len(rows))
         work = self.exchange.start_model()
-        self.exchange.exchange_rows(rows)
         self.opt.step(groups=[1, 2])
         self.exchange.finish(work)
         self.opt.step(groups=[0])

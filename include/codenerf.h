@@ -34,6 +34,9 @@ extern "C" {
 #define CN_ABI_VERSION 2
 #define CN_FP32 0 /* exact-fp32 MFMA path (parity) */
 #define CN_BF16 1 /* bf16 operands, fp32 accumulate (throughput) */
+/* error-compensated bf16: weights and chain operands as bf16 hi + lo pairs,
+ * three MFMAs per block into fp32 (~16-bit operands); dW as CN_BF16 */
+#define CN_BF16X3 2
 /* Largest sample count (M, act_M, R * N) one call accepts: the kernels index
  * samples with 32-bit integers (3 m, 4 m).  Larger images are rendered in
  * ray parts (codenerf_amd.render.ImageStep / CodeNeRF.forward split

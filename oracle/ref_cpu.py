@@ -82,37 +82,70 @@ def positional_encoding(x, n_freq):
 # and the sigma head run in fp32 there (latent.hip; the sigma head reads the
 # fp32 accumulator), so they stay fp32 here.  Off by default: the oracle is
 # the fp32 reference; ``bf16_operands()`` switches a block of code over.
-_BF16 = {"on": False}
+#
+# ``split_w`` restates the error-compensated mode ("bf16x2", precision
+# "bf16s"): every weight is carried as W_hi + W_lo (two bf16, W_hi = rn(W),
+# W_lo = rn(W - W_hi)) and both halves multiply the same bf16 operand into
+# one fp32 accumulator, in the forward and in dX; dW is unchanged.
+# ``split_x`` / ``split_dy`` additionally split the layer inputs / upstream
+# gradients the same way.  ``ops`` sets each operand separately, for the
+# emulation probes (tools/split_emu.py): keys fw_w, fw_x (forward), bw_w,
+# bw_dy (dX), dw_x, dw_dy (dW); values "b" (bf16), "s" (hi + lo), "f" (fp32).
+_OPS_BF16 = dict(fw_w="b", fw_x="b", bw_w="b", bw_dy="b", dw_x="b", dw_dy="b")
+_BF16 = {"on": False, "ops": dict(_OPS_BF16)}
 
 
 def _rb(t):
     return t.to(torch.bfloat16).to(torch.float32)
 
 
+def _q(t, how):
+    """t as an operand: "b" bf16-rounded, "s" hi + lo bf16 pair summed in
+    fp32 (exact: <= 16 significant bits), "f" unchanged."""
+    if how == "f":
+        return t
+    hi = _rb(t)
+    return hi + _rb(t - hi) if how == "s" else hi
+
+
 class _Bf16Linear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
-        xb, wb = _rb(x), _rb(w)
-        ctx.save_for_backward(xb, wb)
-        return xb @ wb.t() + b
+        o = _BF16["ops"]
+        ctx.save_for_backward(x, w)
+        return _q(x, o["fw_x"]) @ _q(w, o["fw_w"]).t() + b
 
     @staticmethod
     def backward(ctx, dy):
-        xb, wb = ctx.saved_tensors
-        d = _rb(dy)
-        d2, x2 = d.reshape(-1, d.shape[-1]), xb.reshape(-1, xb.shape[-1])
-        return d @ wb, d2.t() @ x2, d2.sum(0)
+        x, w = ctx.saved_tensors
+        o = _BF16["ops"]
+        dx = _q(dy, o["bw_dy"]) @ _q(w, o["bw_w"])
+        d2 = _q(dy, o["dw_dy"]).reshape(-1, dy.shape[-1])
+        x2 = _q(x, o["dw_x"]).reshape(-1, x.shape[-1])
+        return dx, d2.t() @ x2, d2.sum(0)
 
 
 class bf16_operands:
-    """with ref_cpu.bf16_operands(): ... -- the bf16 kernels' arithmetic."""
+    """with ref_cpu.bf16_operands(): ... -- the bf16 kernels' arithmetic;
+    ``bf16_operands(split_w=True)`` the compensated bf16x2 kernels'."""
+
+    def __init__(self, split_w=False, split_x=False, split_dy=False, ops=None):
+        o = dict(_OPS_BF16)
+        if split_w:
+            o.update(fw_w="s", bw_w="s")
+        if split_x:
+            o.update(fw_x="s", dw_x="s")
+        if split_dy:
+            o.update(bw_dy="s", dw_dy="s")
+        o.update(ops or {})
+        self.cfg = {"on": True, "ops": o}
 
     def __enter__(self):
-        self.prev = _BF16["on"]
-        _BF16["on"] = True
+        self.prev = {"on": _BF16["on"], "ops": _BF16["ops"]}
+        _BF16.update(self.cfg)
 
     def __exit__(self, *exc):
-        _BF16["on"] = self.prev
+        _BF16.update(self.prev)
 
 
 def _lin(p, name, x):

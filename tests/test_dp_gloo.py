@@ -49,8 +49,8 @@ def _worker(rank, world, port, out):
         ex.zero()
         obj = object_for(step, rank, world, N_OBJ)
         ref_cpu.image_step(p, st, tt, obj, ro, vd, z, gts[obj], chunk=16)
-        work = ex.start_model()          # async model all-reduce
         ex.exchange_rows([obj])          # all_gather of the touched code rows
+        work = ex.start_model()          # async model all-reduce
         ex.finish(work)
         opt.step()
     flat = torch.cat([t.detach().reshape(-1) for t in list(p.values()) + [st, tt]])
@@ -197,3 +197,46 @@ def test_ray_blocks_cover_the_image():
                 blocks = [dp.ray_block(R, FakeDist(world, r), align=align) for r in range(world)]
                 covered = [i for a, b in blocks for i in range(a, b)]
                 assert covered == list(range(R)), (R, world, align)
+
+
+# ---------------------------------------------------------------- code-row exchange edge cases
+def _rows_worker(rank, world, port, out):
+    """Duplicated rows on one rank and unequal row counts across ranks: every
+    rank's distinct rows are summed once into the dense tables."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from codenerf_amd.dp import GradExchange
+    w = torch.zeros(4, 3, requires_grad=True)
+    st = torch.zeros(6, 5, requires_grad=True)
+    tt = torch.zeros(6, 5, requires_grad=True)
+    ex = GradExchange([w], [st, tt], dist)
+    rows = [1, 1, 2] if rank == 0 else [3]
+    for t in (st, tt):
+        t.grad.copy_(torch.arange(30, dtype=torch.float32).reshape(6, 5) * (rank + 1))
+    ex.exchange_rows(rows)
+    if rank == 0:
+        out.put((st.grad.numpy().copy(), tt.grad.numpy().copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_exchange_rows_dedups_and_pads_unequal_counts():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rows_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    sg, tg = q.get(timeout=240)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    base = np.arange(30, dtype=np.float32).reshape(6, 5)
+    want = np.zeros((6, 5), np.float32)
+    want[1] = base[1]            # rank 0's rows 1 (once) and 2
+    want[2] = base[2]
+    want[3] = 2 * base[3]        # rank 1's row 3 (its grads are 2x)
+    np.testing.assert_array_equal(sg, want)
+    np.testing.assert_array_equal(tg, want)

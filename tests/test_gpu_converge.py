@@ -108,11 +108,13 @@ def test_early_train_psnr_matches_reference_at_each_precision(tmp_path):
     root = _data(tmp_path)
     A, init = _run(tmp_path, root, "A", "fp32", True, 0, EARLY)
     H, _ = _run(tmp_path, root, "bf16", "bf16", True, 0, EARLY, init)
+    X, _ = _run(tmp_path, root, "bf16x3", "bf16x3", True, 0, EARLY, init)
     ref32 = _replay(root, init, 0, EARLY, bf16=False)
     ref16 = _replay(root, init, 0, EARLY, bf16=True)
     d32 = np.abs(A - ref32)
     prefix = int(np.argmax(d32 > 0.01)) if (d32 > 0.01).any() else EARLY
     d16 = np.abs(H[:prefix] - ref16[:prefix])
+    dx3 = np.abs(X[:prefix] - ref32[:prefix])
     # bf16's own replayable prefix: one bf16 ulp of a stored activation (from
     # an fp32 accumulation-order difference at a rounding boundary) is a 0.4%
     # change, so a bf16 trajectory leaves its replay sooner than fp32 does
@@ -121,12 +123,15 @@ def test_early_train_psnr_matches_reference_at_each_precision(tmp_path):
           f"dB (all {EARLY}: {d32.max():.4f}); HIP bf16 vs bf16-operand replay max |d| {d16.max():.4f} dB; "
           f"HIP bf16 vs fp32 replay max |d| {np.abs(H[:prefix] - ref32[:prefix]).max():.4f} dB (intrinsic, "
           f"bf16-operand replay vs fp32 replay {np.abs(ref16[:prefix] - ref32[:prefix]).max():.4f} dB)")
-    for n, r in (("HIP fp32", A), ("fp32 replay", ref32), ("HIP bf16", H), ("bf16 replay", ref16)):
+    print(f"HIP bf16x3 vs fp32 replay max |d| {dx3.max():.4f} dB over the replayable prefix "
+          f"(all {EARLY}: {np.abs(X - ref32).max():.4f})")
+    for n, r in (("HIP fp32", A), ("fp32 replay", ref32), ("HIP bf16", H), ("bf16 replay", ref16), ("HIP bf16x3", X)):
         print(f"{n:12s}", np.round(r, 3).tolist())
     print(f"bf16 replayable prefix (within 0.05 dB of the bf16-operand replay): {p16} steps")
     assert prefix >= 20                       # fp32: the north-star 0.05 dB (0.01 here) over >= 20 steps
     assert p16 >= 5                           # bf16: within 0.05 dB of its own precision's replay
     assert d16[:p16].max() <= 0.05
+    assert dx3.max() <= 0.05                  # bf16x3: the north-star bar against the FP32 replay
 
 
 @pytest.mark.timeout(900)

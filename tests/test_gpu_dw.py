@@ -114,7 +114,7 @@ def scatter_cols(dw_cols, fn, n_real):
 
 
 @pytest.mark.parametrize("precision,R", [("bf16", 3000 - 7), ("fp32", 3000 - 7), ("bf16", 1), ("fp32", 5),
-                                         ("bf16", 4)])
+                                         ("bf16", 4), ("bf16x3", 3000 - 7)])
 def test_weight_gradients_match_float64_reduction(precision, R):
     """R rays x 64 samples: ragged (191,552 samples), one ray (64 samples: one
     partial 256-sample tile), 5 rays (320) and 4 rays (exactly one tile)."""
@@ -149,8 +149,8 @@ def test_weight_gradients_match_float64_reduction(precision, R):
     torch.cuda.synchronize()
     G = dict(zip(names, grads))
 
-    dtype = torch.bfloat16 if precision == "bf16" else torch.float32
-    es = 2 if precision == "bf16" else 4
+    dtype = torch.float32 if precision == "fp32" else torch.bfloat16     # bf16x3 stores bf16 planes too
+    es = 4 if precision == "fp32" else 2
     off = act_offsets(Mp, es)
     Y = [decode(act, off[f"Y{p}"], plane_width(p), Mp, dtype) if plane_width(p) else None for p in range(N_PLANES)]
     dA = [decode(act, off[f"dA{p}"], dplane_width(p), Mp, dtype) if dplane_width(p) else None

@@ -137,10 +137,13 @@ def test_crop_phase_and_two_instances_match_cpu_replay(tmp_path):
         assert d.max() <= 2 * 6e-4 and np.mean(d <= 1e-6 + 1e-3 * np.abs(v.detach().numpy())) > 0.99, k
 
 
-def test_bf16_train_psnr_within_005db_of_fp32_replay(tmp_path):
-    """north_star: "PSNR within 0.05 dB of reference" for the bf16 (C2) path:
-    the bf16-MFMA trainer against the fp32 CPU replay of the reference loop
-    on the same data, initial weights and RNG draws."""
+def test_bf16_trainer_first_steps_near_init_track_fp32_replay(tmp_path):
+    """Plumbing check of the bf16 trainer: its first 8 iterations from random
+    init (PSNRs of a few dB) against the fp32 CPU replay of the reference
+    loop on the same data, initial weights and RNG draws.  NOT the
+    north-star PSNR bar -- that is tests/test_gpu_regime.py (the reference's
+    optimiser regime) and tests/test_gpu_converge.py (bf16x3 against the fp32
+    replay on a converging trajectory)."""
     from codenerf_amd.data import make_synthetic_srn
     from codenerf_amd.trainer import Trainer
     root = str(tmp_path / "data")
