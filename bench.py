@@ -61,7 +61,9 @@ def parse():
     #   c4: optimize.py test-time code optimisation, 50 views x 128^2 x 64
     #       samples per step, fwd + dX only (no weight gradients), bf16
     #   c5: 256^2, 128 + 128 samples, fp32, the image in 8 ray parts
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
+    #   c4eval: optimize.py's evaluation loop (src/optimizer.py:108-130): one
+    #       step = one 128^2 view x 64 samples rendered forward-only + MSE
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c4eval", "c5"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-overlap", action="store_true",
                     help="one dX launch then one dW launch (no two-stream dX / dW pipelining)")
@@ -165,7 +167,7 @@ def build_workload(args, dev, rank, world, precision, timers, dist):
     from codenerf_amd.data import _object_spec, _render_object
     g = torch.Generator(device="cpu").manual_seed(99 + rank)
     spec = _object_spec(np.random.Generator(np.random.PCG64(99 + rank)))
-    n_views = 50 if args.config == "c4" else 8
+    n_views = 50 if args.config in ("c4", "c4eval") else 8
 
     def view():
         c2w = make_pose(radius, float(torch.rand(1, generator=g)) * 360 - 180,
@@ -197,6 +199,28 @@ def build_workload(args, dev, rank, world, precision, timers, dist):
                 views.append(loss)
             copt.step()
             last["losses"] = torch.cat(views)
+    elif args.config == "c4eval":
+        # src/optimizer.py:108-130: no_grad forward of a held-out view with
+        # the optimised codes, composite, MSE (PSNR); the view rays come from
+        # the pose on the device (get_rays), z from the host draw
+        from codenerf_amd import engine as _eng
+        eng = model.engine()
+        params = model.param_list()
+        eng.ensure_packed(params, bwd=False)
+        blob, _ = eng.latent_fwd(params, shape_codes.detach()[0], texture_codes.detach()[0])
+        M = R * args.n_coarse
+        sig = torch.empty(eng.pad(M), device=dev)
+        rgbs = torch.empty(eng.pad(M), 3, device=dev)
+
+        def step(i):
+            v = i % n_views
+            ro, vd = _eng.get_rays_dev(H, W, focal, True, poses[v])
+            z = core.stratified_z(dev)
+            ev = timers.mark("fwd")
+            eng.mlp_fwd(blob, M, rays_o=ro, rays_d=vd, z=z, n_samples=args.n_coarse, sigma=sig, rgb=rgbs)
+            timers.done("fwd", ev, n=M)
+            rgb, _ = _eng.composite_fwd(sig, rgbs, z, R, args.n_coarse)
+            last["losses"] = ((rgb - gts[v]) ** 2).mean().reshape(1)
     else:
         def step(i):
             v = i % n_views
@@ -240,8 +264,8 @@ def timed_run(wl, steps, warmup, timers, dist, dev):
 
 def main():
     args = parse()
-    if args.config == "c4":
-        args.H, args.n_coarse, args.n_fine, args.precision = 128, 64, 0, "bf16"
+    if args.config in ("c4", "c4eval"):
+        args.H, args.n_coarse, args.n_fine = 128, 64, 0
     elif args.config == "c5":
         args.H, args.n_coarse, args.n_fine, args.precision = 256, 128, 128, "fp32"
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -291,6 +315,7 @@ def main():
     if rank == 0:
         metric = {"c2": "ray-samples/sec (train step), SRN-cars 128x128, 64 coarse + 64 fine samples",
                   "c4": "ray-samples/sec (optimize.py code optimisation step), 50 views x 128x128 x 64 samples",
+                  "c4eval": "ray-samples/sec (optimize.py evaluation: forward-only render + MSE), 128x128 x 64 samples per view",
                   "c3": "ray-samples/sec (train step), SRN-chairs geometry 128x128, 64 coarse + 64 fine samples",
                   "c5": "ray-samples/sec (train step), SRN-cars 256x256, 128 coarse + 128 fine samples, fp32"}
         out = {
@@ -302,8 +327,9 @@ def main():
             "data": f"synthetic ({H}x{H} ray-cast ellipsoid object per rank, poses on a radius-{radius} sphere, "
                     f"random-init weights)",
             "config": {"workload": f"{'srnchair' if args.config == 'c3' else 'srncar'}.json net, {H}x{H} image/object/step, {args.n_coarse}+{args.n_fine} "
-                                   f"samples/ray, " + ("50 views, codes-only fwd+dX+AdamW" if args.config == "c4"
-                                                       else "train step incl. AdamW"),
+                                   f"samples/ray, " + {"c4": "50 views, codes-only fwd+dX+AdamW",
+                                                       "c4eval": "one held-out view per step, forward-only + MSE"}.get(
+                                       args.config, "train step incl. AdamW"),
                        "name": args.config, "objects_per_step": world,
                        "rays_per_step_per_gpu": R, "parallelism": f"dp{world}"},
             "roofline": roof,
@@ -366,11 +392,16 @@ def roofline(args, timers, samples_per_step, ms, overlapped):
         return None
     per_step = {k: v[1] / args.steps for k, v in summ.items()}    # ms per step (all launches)
     launches = {k: len(timers.ev[k]) / args.steps for k in timers.ev}
-    kinds = [k for k in FLOP_PER_SAMPLE if k in summ and not (k == "dw" and args.config == "c4")]
+    passes = {"c4": ("fwd", "bwd"), "c4eval": ("fwd",)}.get(args.config, ("fwd", "bwd", "dw"))
+    kinds = [k for k in FLOP_PER_SAMPLE if k in summ and k in passes]
     kernels = {}
     for k in kinds:
         r = kernel_roofline(k, args.precision, timers, load_traffic(args.config, k, args.precision))
         if r is not None:
+            if args.config == "c4eval":
+                r["kernel"] = "chain_kernel<fwd,infer>"
+            elif args.config == "c4":
+                r["kernel"] = {"fwd": "chain_kernel<fwd,codes>", "bwd": "chain_kernel<bwd,codes>"}[k]
             r["launches_per_step"] = launches[k]
             r["ms_per_step"] = round(per_step[k], 4)
             kernels[k] = r
@@ -381,11 +412,11 @@ def roofline(args, timers, samples_per_step, ms, overlapped):
     roof = {"bound": d["bound"], "kernel": d["kernel"], "achieved": d["achieved"], "peak": d["peak"],
             "unit": d["unit"], "frac": d["frac"], "traffic": d["traffic"], "basis": d["basis"],
             "ms_per_launch_uncontended": d["ms_per_launch"], "kernels": kernels}
-    if overlapped and args.config != "c4":
+    if overlapped and "dw" in passes:
         roof["overlap"] = ("dX chain of row range i on the main stream || dW of range i-1 on a side stream; "
                            "per-kernel spans overlap, so their sum exceeds the step")
     peak = FP32_PEAK_TFLOPS if args.precision == "fp32" else BF16_PEAK_TFLOPS
-    step_flops = sum(v for k, v in FLOP_PER_SAMPLE.items() if args.config != "c4" or k != "dw") * samples_per_step
+    step_flops = sum(v for k, v in FLOP_PER_SAMPLE.items() if k in passes) * samples_per_step
     roof["step"] = {"achieved": round(step_flops / (ms * 1e-3) / 1e12, 2), "unit": "TFLOP/s",
                     "frac": round(step_flops / (ms * 1e-3) / 1e12 / peak, 4)}
     return roof
@@ -417,6 +448,27 @@ def cpu_model():
 
 
 def cpu_baseline(threads, args):
+    """The oracle sample below at the box's thread counts: the process's
+    OMP_NUM_THREADS share (16 on the GPU box), the CPUs it may run on
+    (sched_getaffinity) and every host CPU (os.cpu_count()); ``value`` /
+    ``cores`` are the fastest, every count is listed under ``by_threads``."""
+    if threads is not None:
+        return _cpu_baseline_at(threads, args, 10.0)
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0")) or None
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = None
+    counts = sorted({c for c in (omp, aff, os.cpu_count()) if c})
+    runs = [_cpu_baseline_at(c, args, 8.0 if len(counts) > 1 else 10.0) for c in counts]
+    best = dict(max(runs, key=lambda r: r["value"]))
+    best["by_threads"] = {r["cores"]: r["value"] for r in runs}
+    best["affinity_cpus"] = aff
+    best["omp_num_threads"] = omp
+    return best
+
+
+def _cpu_baseline_at(threads, args, seconds):
     """The CPU oracle (torch fp32 restatement of the reference, pinned to its
     golden vectors) on a bounded sample of the SAME step: 1024 rays x
     (n_coarse stratified + n_fine importance) samples -- coarse forward,
@@ -426,8 +478,6 @@ def cpu_baseline(threads, args):
     sys.path.insert(0, os.path.join(REPO, "tests"))
     from oracle import ref_cpu
     from oracle.params import make_params
-    if threads is None:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
     torch.set_num_threads(threads)
     p = ref_cpu.param_tensors(make_params(0))
     n_obj = args.objects
@@ -439,12 +489,20 @@ def cpu_baseline(threads, args):
     z = ref_cpu.stratified_z(0.8, 1.8, Nc)
     gt = torch.rand(B, 3)
     codes_only = args.config == "c4"
+    eval_only = args.config == "c4eval"
     groups = [([st], 1e-3), ([tt], 1e-3)] if codes_only else [(list(p.values()), 1e-4), ([st], 1e-3), ([tt], 1e-3)]
     opt = ref_cpu.AdamWRef(groups)
 
     def one():
         for t in list(p.values()) + [st, tt]:
             t.grad = None
+        if eval_only:
+            with torch.no_grad():
+                xyz = ro[:, None, :] + vd[:, None, :] * z[:, None]
+                sig, rgbs = ref_cpu.codenerf_forward(p, xyz, vd[:, None, :].expand(-1, Nc, -1), st[0][None], tt[0][None])
+                rgb, _ = ref_cpu.volume_rendering(sig, rgbs, z)
+                ((rgb - gt) ** 2).mean()
+            return
         if Nf:
             with torch.no_grad():
                 xyz = ro[:, None, :] + vd[:, None, :] * z[:, None]
@@ -457,17 +515,19 @@ def cpu_baseline(threads, args):
 
     one()
     reps, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < 10.0 or reps < 2:
+    while time.perf_counter() - t0 < seconds or reps < 2:
         one()
         reps += 1
     dt = time.perf_counter() - t0
-    what = "codes-only fwd+composite+MSE+backward+AdamW(codes)" if codes_only else \
+    what = "forward + composite + MSE (no grad)" if eval_only else \
+        "codes-only fwd+composite+MSE+backward+AdamW(codes)" if codes_only else \
         ("coarse fwd + sample_pdf + fine fwd + merged composite + MSEs + backward + AdamW(model, code tables)"
          if Nf else "fwd+composite+MSE+backward+AdamW")
     return {"value": round(B * (Nc + Nf) * reps / dt, 1), "unit": "ray-samples/s", "cores": threads,
             "host_cpus": os.cpu_count(), "cpu_model": cpu_model(), "kind": "port",
             "sample": f"{reps} x ({B} rays x {Nc}+{Nf} samples) {what}, torch CPU fp32 oracle "
-                      f"(oracle/ref_cpu.py; the coarse forward runs twice, once without grad for sample_pdf), {threads} threads"}
+                      f"(oracle/ref_cpu.py" + ("; the coarse forward runs twice, once without grad for sample_pdf" if Nf else "")
+                      + f"), {threads} threads"}
 
 
 if __name__ == "__main__":

@@ -70,6 +70,7 @@ _SIGS = {
     "cn_render_loss_fine": (_I, [_P, _P, _P, _I, _I, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P,
                                  _P]),
     "cn_adamw_step": (_I, [_I, _P, _P, _P, _P, _P, _P, _D, _D, _D, _D, _I, _P]),
+    "cn_adamw_step_zero_grad": (_I, [_I, _P, _P, _P, _P, _P, _P, _D, _D, _D, _D, _I, _P]),
 }
 
 EXPORTED = tuple(_SIGS)

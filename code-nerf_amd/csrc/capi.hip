@@ -459,9 +459,9 @@ int cn_render_loss_fine(const float* d_sigma_c, const float* d_rgb_c, const floa
   return launch_check("chunk_loss_kernel");
 }
 
-int cn_adamw_step(int nseg, float* const* p, const float* const* g, float* const* m, float* const* v,
-                  const int* n, const double* lr, double wd, double beta1, double beta2, double eps, int step,
-                  void* stream) {
+static int adamw_impl(int nseg, float* const* p, float* const* g, float* const* m, float* const* v, const int* n,
+                      const double* lr, double wd, double beta1, double beta2, double eps, int step, int zero_grad,
+                      void* stream) {
   if (nseg <= 0 || !p || !g || !m || !v || !n || !lr) return fail("cn_adamw_step: bad argument");
   if (step < 1) return fail("cn_adamw_step: step must be >= 1");
   const double bc1 = 1.0 - std::pow(beta1, step);
@@ -482,11 +482,24 @@ int cn_adamw_step(int nseg, float* const* p, const float* const* g, float* const
     a.one_m_beta2 = (float)(1.0 - beta2);
     a.bc2_sqrt = (float)std::sqrt(bc2);
     a.eps = (float)eps;
+    a.zero_grad = zero_grad;
     const int grid = std::min(2048, grid_for(total, 256));
     hipLaunchKernelGGL(adamw_kernel, dim3(grid), dim3(256), 0, S(stream), a);
     if (launch_check("adamw_kernel")) return -1;
   }
   return 0;
+}
+
+int cn_adamw_step(int nseg, float* const* p, const float* const* g, float* const* m, float* const* v,
+                  const int* n, const double* lr, double wd, double beta1, double beta2, double eps, int step,
+                  void* stream) {
+  return adamw_impl(nseg, p, const_cast<float* const*>(g), m, v, n, lr, wd, beta1, beta2, eps, step, 0, stream);
+}
+
+int cn_adamw_step_zero_grad(int nseg, float* const* p, float* const* g, float* const* m, float* const* v,
+                            const int* n, const double* lr, double wd, double beta1, double beta2, double eps,
+                            int step, void* stream) {
+  return adamw_impl(nseg, p, g, m, v, n, lr, wd, beta1, beta2, eps, step, 1, stream);
 }
 
 }  // extern "C"

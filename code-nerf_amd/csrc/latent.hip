@@ -66,6 +66,8 @@ __global__ __launch_bounds__(256) void latent_bwd_kernel(LatentBwdArgs a) {
   const int j = blockIdx.x;
   const int rb = blockIdx.y;
   const int i = threadIdx.x;
+  // code_grad_kernel (next on the stream) adds both codes' regulariser terms
+  if (j == 0 && rb == 0 && i == 0 && a.reg_out) *a.reg_out = 0.f;
   const bool shape = j < SB;
   const int wl = shape ? P.shape_w(j) : P.tex_w(j - SB);          // layer fed by z_j
   const int lw = shape ? P.shape_latent_w(j) : P.tex_latent_w(j - SB);

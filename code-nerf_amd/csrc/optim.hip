@@ -31,7 +31,7 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* const* params, c
 constexpr int kAdamMaxSeg = 48;
 struct AdamSeg {
   float* p;
-  const float* g;
+  float* g;
   float* m;
   float* v;
   int n;
@@ -46,6 +46,7 @@ struct AdamArgs {
   float beta2, one_m_beta2;
   float bc2_sqrt;     // sqrt(1 - beta2^t)
   float eps;
+  int zero_grad;      // write g = 0 after reading it (the next step's zero_grad, for free)
 };
 
 __global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a) {
@@ -68,6 +69,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a) {
     s.p[i] = p;
     s.m[i] = m;
     s.v[i] = v;
+    if (a.zero_grad) s.g[i] = 0.f;
   }
 }
 

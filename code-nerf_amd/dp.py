@@ -66,15 +66,23 @@ class GradExchange:
         for t in self.tables:
             t.grad = torch.zeros_like(t)
         self.dist, self.group = dist, group
+        self.clean = True        # every gradient is known to be 0 (zero() is then a no-op)
 
     @property
     def active(self):
         return _active(self.dist, self.group)
 
     def zero(self):
+        if self.clean:
+            return
         self.bucket.zero()
         for t in self.tables:
             t.grad.zero_()
+        self.clean = True
+
+    def mark_dirty(self):
+        """A backward wrote into the gradients: the next zero() must clear them."""
+        self.clean = False
 
     def start_model(self):
         """Launch the model-gradient all-reduce; returns a handle for finish()."""

@@ -271,7 +271,8 @@ def sample_points(ro, vd, z, R, N):
     return xyz, vrep
 
 
-def adamw_step(params, grads, exp_avgs, exp_avg_sqs, lrs, weight_decay, beta1, beta2, eps, step):
+def adamw_step(params, grads, exp_avgs, exp_avg_sqs, lrs, weight_decay, beta1, beta2, eps, step, zero_grad=False):
+    """zero_grad: the kernel also sets every gradient to 0 after reading it."""
     L = _lib.lib()
     n = len(params)
     P = ctypes.c_void_p * n
@@ -285,9 +286,10 @@ def adamw_step(params, grads, exp_avgs, exp_avg_sqs, lrs, weight_decay, beta1, b
     ptrs = lambda ts: arr([t.data_ptr() for t in ts], ctypes.c_void_p)
     counts = arr([t.numel() for t in params], ctypes.c_int)
     lr = arr([float(x) for x in lrs], ctypes.c_double)
-    check(L.cn_adamw_step(n, ptrs(params), ptrs(grads), ptrs(exp_avgs), ptrs(exp_avg_sqs), counts, lr,
-                          float(weight_decay), float(beta1), float(beta2), float(eps), int(step),
-                          _dev_stream(params[0])), "cn_adamw_step")
+    fn = L.cn_adamw_step_zero_grad if zero_grad else L.cn_adamw_step
+    check(fn(n, ptrs(params), ptrs(grads), ptrs(exp_avgs), ptrs(exp_avg_sqs), counts, lr,
+             float(weight_decay), float(beta1), float(beta2), float(eps), int(step),
+             _dev_stream(params[0])), "cn_adamw_step")
     # the kernel wrote the tensors behind torch's back: bump their version
     # counters so version-keyed caches (the packed weights) see the update
     increment_version(list(params))

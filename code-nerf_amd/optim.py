@@ -31,10 +31,12 @@ class FusedAdamW:
                         p.grad.zero_()
 
     @torch.no_grad()
-    def step(self, groups=None):
+    def step(self, groups=None, zero_grad=False):
         """groups: indices of the param groups to update (default all) -- a
         step split over two calls (codes while the model gradients are still
-        being all-reduced, then the model) is the same update as one call."""
+        being all-reduced, then the model) is the same update as one call.
+        zero_grad: the update kernel leaves every gradient it read at 0 (the
+        next zero_grad() for free)."""
         # one launch per (betas, eps, weight_decay) combination; lr is per tensor
         buckets = {}
         sel = self.param_groups if groups is None else [self.param_groups[i] for i in groups]
@@ -51,4 +53,4 @@ class FusedAdamW:
         for ((betas, eps, wd), step), items in buckets.items():
             _eng.adamw_step([p for p, _, _ in items], [p.grad for p, _, _ in items],
                             [s["exp_avg"] for _, s, _ in items], [s["exp_avg_sq"] for _, s, _ in items],
-                            [lr for _, _, lr in items], wd, betas[0], betas[1], eps, step)
+                            [lr for _, _, lr in items], wd, betas[0], betas[1], eps, step, zero_grad=zero_grad)

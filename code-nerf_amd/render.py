@@ -65,11 +65,22 @@ class ImageStep:
                       rgb=torch.empty(cap, 3, dtype=torch.float32, device=dev),
                       dsig=torch.empty(cap, dtype=torch.float32, device=dev),
                       drgb=torch.empty(cap, 3, dtype=torch.float32, device=dev))
-            if self.recompute:      # outputs of the recompute forward (discarded)
-                ws.update(dsig_tmp=torch.empty(cap, dtype=torch.float32, device=dev),
-                          drgb_tmp=torch.empty(cap, 3, dtype=torch.float32, device=dev))
             self._ws[eng.device] = ws
         return ws
+
+    @staticmethod
+    def _zero_pad_rows(ws, layout, ranges):
+        """Upstream-gradient rows no loss kernel writes (the padding between
+        and after the coarse and fine row ranges) must be 0 for the dX chain.
+        They are zeroed when the row layout changes, not every step: nothing
+        else writes them."""
+        if ws.get("pad_layout") == layout:
+            return
+        for a, b in ranges:
+            if b > a:
+                ws["dsig"][a:b].zero_()
+                ws["drgb"][a:b].zero_()
+        ws["pad_layout"] = layout
 
     def side_stream(self, device):
         s = self._side.get(device)
@@ -190,8 +201,7 @@ class ImageStep:
         if tm:
             tm.done("fwd", ev, n=M)
         dsig, drgb = ws["dsig"], ws["drgb"]
-        dsig[M:Mp].zero_()
-        drgb[M:Mp].zero_()
+        self._zero_pad_rows(ws, ("coarse", M), [(M, Mp)])
         out_rgb, chunk_loss, _, _ = _eng.render_loss(sigma, rgb, z, R, N, gt, self.chunk, self.white_bg,
                                                      dsig=dsig[:M], drgb=drgb[:M])
         if weight_grads:
@@ -206,7 +216,7 @@ class ImageStep:
             if tm:
                 tm.done("dw", ev, n=M)
             grads = ws.setdefault("scratch_grads", [torch.zeros_like(p) for p in params])
-        reg_out = torch.zeros(1, dtype=torch.float32, device=eng.device)
+        reg_out = torch.empty(1, dtype=torch.float32, device=eng.device)     # written by cn_latent_bwd
         eng.latent_bwd(params, grads, s, t, zvec, ws["dbuf"], shape_table.grad[obj_idx],
                        texture_table.grad[obj_idx], self.reg_coef if reg else 0.0, reg_out)
         return chunk_loss, out_rgb, reg_out
@@ -255,8 +265,7 @@ class ImageStep:
         ws = self._workspace(eng, M)
         cap = ws["cap"]
         sig, rgb, dsig, drgb = ws["sig"], ws["rgb"], ws["dsig"], ws["drgb"]
-        dsig[:Mp].zero_()
-        drgb[:Mp].zero_()
+        self._zero_pad_rows(ws, ("fine", Mc, Mf), [(Mc, Mc_p), (Mc_p + Mf, Mp)])
         eng.ensure_packed(params, bwd=True)
         s, t = shape_table.detach()[obj_idx], texture_table.detach()[obj_idx]
         blob, zvec = eng.latent_fwd(params, s, t)
@@ -287,6 +296,9 @@ class ImageStep:
             # recompute A/B (hard part 2): the forward passes above
             # stored only ReLU masks + sigma pre-activations; the planes the dW
             # pass reads are produced here by a second training forward
+            if ws.get("dsig_tmp") is None or ws["dsig_tmp"].numel() < cap:   # its (discarded) outputs
+                ws["dsig_tmp"] = torch.empty(cap, dtype=torch.float32, device=eng.device)
+                ws["drgb_tmp"] = torch.empty(cap, 3, dtype=torch.float32, device=eng.device)
             ev = tm.mark("fwd") if tm else None
             eng.mlp_fwd(blob, Mc, rays_o=rays_o, rays_d=viewdirs, z=z_c, z_stride=0 if z_c.dim() == 1 else Nc,
                         n_samples=Nc, act=ws["act"], act_M=cap, act_row0=0, sigma=ws["dsig_tmp"][:Mc_p],
@@ -296,7 +308,7 @@ class ImageStep:
             if tm:
                 tm.done("fwd", ev)
         self._bwd_dw(eng, blob, ws, zvec, eng.table(grads), M)
-        reg_out = torch.zeros(1, dtype=torch.float32, device=eng.device)
+        reg_out = torch.empty(1, dtype=torch.float32, device=eng.device)     # written by cn_latent_bwd
         eng.latent_bwd(params, grads, s, t, zvec, ws["dbuf"], shape_table.grad[obj_idx],
                        texture_table.grad[obj_idx], self.reg_coef if reg else 0.0, reg_out)
         self.last_z_f = z_f

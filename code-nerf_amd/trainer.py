@@ -116,11 +116,13 @@ class Trainer:
                 else:
                     loss_per_img, rgb, reg = self.step_impl.forward_backward(
                         rays_o, viewdir, z, gt, self.shape_codes.weight, self.texture_codes.weight, oi)
+                self.exchange.mark_dirty()                          # the next zero() must clear them
             self.exchange.exchange_rows([oi], 1)          # data parallel: the touched code rows,
             work = self.exchange.start_model()           # then the async model all-reduce
-            self.opts.step(groups=[1, 2])
+            self.opts.step(groups=[1, 2], zero_grad=True)  # the kernel leaves the gradients at 0:
             self.exchange.finish(work)
-            self.opts.step(groups=[0])
+            self.opts.step(groups=[0], zero_grad=True)
+            self.exchange.clean = True                     # the next zero_grad needs no launch
             mse = float(loss_per_img.mean())
             self.log_psnr_time(mse, time.time() - t1, oi, float(reg))
             if self.check_iter and self.niter % self.check_iter == 0:

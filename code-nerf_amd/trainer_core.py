@@ -19,7 +19,7 @@ from .render import ImageStep
 
 class TrainCore:
     def __init__(self, model, shape_codes, texture_codes, near, far, n_coarse, n_fine=0, chunk=2048,
-                 reg_coef=1e-4, lr=(1e-4, 1e-3), timers=None, dist=None, step_opts=None):
+                 reg_coef=1e-4, lr=(1e-4, 1e-3), timers=None, dist=None, step_opts=None, zero_grad_in_adamw=True):
         self.model = model
         self.shape_codes = shape_codes
         self.texture_codes = texture_codes
@@ -31,15 +31,22 @@ class TrainCore:
         self.exchange = GradExchange(model.param_list(), [shape_codes, texture_codes], dist)
         self.bucket = self.exchange.bucket
         self.flat_grad = self.bucket.flat
+        # the AdamW kernel leaves the gradients it consumed at 0, so the next
+        # step's zero_grad costs no launch (False keeps .grad readable after
+        # train_step, for tests)
+        self.zero_grad_in_adamw = bool(zero_grad_in_adamw)
         self.opt = FusedAdamW([{"params": model.param_list(), "lr": lr[0]},
                                {"params": [shape_codes], "lr": lr[1]},
                                {"params": [texture_codes], "lr": lr[1]}])
 
     def stratified_z(self, device):
+        """src/utils.py:24-29 on the host, as the reference draws it (global
+        CPU generator): one (N,) vector, copied to the device (no kernel)."""
         n = self.n_coarse
         half = (self.far - self.near) / (2 * n)
-        z = torch.linspace(self.near + half, self.far - half, n, device=device)
-        return z + torch.rand(n, device=device) * (self.far - self.near) / (2 * n)
+        z = torch.linspace(self.near + half, self.far - half, n)
+        z = z + torch.rand(n) * (self.far - self.near) / (2 * n)
+        return z.pin_memory().to(device, non_blocking=True)
 
     def train_step(self, H, W, focal, c2w, gt, obj):
         """One object step: rays, stratified z, the image forward/backward
@@ -50,7 +57,7 @@ class TrainCore:
         dev = c2w.device
         ro, vd = _eng.get_rays_dev(H, W, focal, True, c2w)
         z = self.stratified_z(dev)
-        self.exchange.zero()
+        self.exchange.zero()           # no launch when the last AdamW step left the gradients at 0
         if self.n_fine:
             rand_f = torch.rand(H * W, self.n_fine, device=dev)
             loss_c, loss_f, rgb, _ = self.step_impl.forward_backward_fine(
@@ -69,8 +76,12 @@ class TrainCore:
         the model bucket's all-reduce is issued asynchronously and the code
         tables take their AdamW step while it is in flight; then the model's
         AdamW step."""
+        self.exchange.mark_dirty()     # a backward filled the gradients
         self.exchange.exchange_rows(rows, len(rows))
         work = self.exchange.start_model()
-        self.opt.step(groups=[1, 2])
+        zg = self.zero_grad_in_adamw
+        self.opt.step(groups=[1, 2], zero_grad=zg)
         self.exchange.finish(work)
-        self.opt.step(groups=[0])
+        self.opt.step(groups=[0], zero_grad=zg)
+        if zg:
+            self.exchange.clean = True

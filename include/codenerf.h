@@ -220,6 +220,11 @@ int cn_render_loss_fine(const float *d_sigma_c, const float *d_rgb_c, const floa
 int cn_adamw_step(int nseg, float *const *p, const float *const *g, float *const *m,
                   float *const *v, const int *n, const double *lr, double weight_decay,
                   double beta1, double beta2, double eps, int step, void *stream);
+/* the same step, and every gradient element is set to 0 once read: the next
+ * step's optimizer.zero_grad() (src/trainer.py:64) without a launch of its own */
+int cn_adamw_step_zero_grad(int nseg, float *const *p, float *const *g, float *const *m,
+                            float *const *v, const int *n, const double *lr, double weight_decay,
+                            double beta1, double beta2, double eps, int step, void *stream);
 
 #ifdef __cplusplus
 }

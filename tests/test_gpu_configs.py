@@ -304,6 +304,77 @@ def test_c4_codes_only_50_views_vs_oracle():
     np.testing.assert_allclose(l16.numpy(), losses.numpy(), rtol=2e-3)
 
 
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("precision", ["bf16", "bf16x3"])
+def test_c4_full_size_50_views_properties_and_ray_subset(precision):
+    """C4 at BASELINE's size: 50 views x 128^2 rays x 64 samples (52.4 M
+    samples) of codes-only optimisation (src/optimizer.py:73-97).  Full size:
+    the step's code gradient equals the view-by-view sum (linearity, same
+    accumulation order: bitwise), losses finite, and three AdamW code steps
+    lower the 50-view loss.  A 2,048-ray subset of view 0 against the oracle
+    at the same operand precision (ref_cpu.bf16_operands)."""
+    from codenerf_amd import engine as _eng
+    from codenerf_amd.optim import FusedAdamW
+    from codenerf_amd.render import ImageStep
+    H, N, n_views = 128, 64, 50
+    dev = _dev()
+    params = make_params(32)
+    s0, t0 = make_codes(32, 1)
+    focal, views = _c4_views(H, n_views, 32)
+    z = _z(0.8, 1.8, N, 6).to(dev)
+    m = _model(params, precision)
+    step = ImageStep(m, chunk=2048, reg_coef=1e-4)
+    rays = [(*_eng.get_rays_dev(H, H, focal, True, c2w.to(dev)), gt.to(dev)) for c2w, gt in views]
+    sc = torch.nn.Parameter(torch.tensor(s0, device=dev))
+    tc = torch.nn.Parameter(torch.tensor(t0, device=dev))
+
+    def full_step():
+        sc.grad, tc.grad = torch.zeros_like(sc), torch.zeros_like(tc)
+        ls = [step.forward_backward(ro, vd, z, gt, sc, tc, 0, weight_grads=False)[0] for ro, vd, gt in rays]
+        return torch.cat(ls)
+
+    l0 = full_step()
+    g_all = (sc.grad.clone(), tc.grad.clone())
+    # view by view, summed in the same order
+    acc = [torch.zeros_like(sc), torch.zeros_like(tc)]
+    for ro, vd, gt in rays:
+        sc.grad, tc.grad = torch.zeros_like(sc), torch.zeros_like(tc)
+        step.forward_backward(ro, vd, z, gt, sc, tc, 0, weight_grads=False)
+        acc[0] += sc.grad
+        acc[1] += tc.grad
+    torch.cuda.synchronize()
+    assert torch.isfinite(l0).all() and l0.numel() == n_views * (H * H // 2048)
+    assert torch.equal(g_all[0], acc[0]) and torch.equal(g_all[1], acc[1])
+    opt = FusedAdamW([{"params": [sc], "lr": 1e-2}, {"params": [tc], "lr": 1e-2}])
+    means = [float(l0.mean())]
+    for _ in range(3):
+        full_step()
+        opt.step()
+        means.append(float(full_step().mean()))
+    print(f"\nC4 {precision}: 50-view mean loss over 3 code steps {np.round(means, 5).tolist()}")
+    assert means[-1] < means[0]
+    # 2,048 rays of view 0 vs the oracle at the same operand precision
+    a, b = 4096, 6144
+    ro, vd, gt = rays[0]
+    sc.data.copy_(torch.tensor(s0, device=dev))
+    tc.data.copy_(torch.tensor(t0, device=dev))
+    sc.grad, tc.grad = torch.zeros_like(sc), torch.zeros_like(tc)
+    l_sub, rgb_sub, _ = step.forward_backward(ro[a:b], vd[a:b], z, gt[a:b], sc, tc, 0, weight_grads=False)
+    torch.cuda.synchronize()
+    p = ref_cpu.param_tensors(params, requires_grad=False)
+    rs = torch.tensor(s0, requires_grad=True)
+    rt = torch.tensor(t0, requires_grad=True)
+    ops = {} if precision == "bf16" else dict(ops=dict(fw_w="s", fw_x="s", bw_w="s", bw_dy="s"))
+    with ref_cpu.bf16_operands(**ops):
+        l_r, rgb_r = ref_cpu.image_step(p, rs, rt, 0, ro[a:b].cpu(), vd[a:b].cpu(), z.cpu(), gt[a:b].cpu(),
+                                        chunk=2048, reg_coef=1e-4)
+    tol = 2e-3 if precision == "bf16" else 2e-5
+    assert float((rgb_sub.cpu() - rgb_r).abs().max()) <= tol
+    np.testing.assert_allclose(l_sub.cpu().numpy(), np.array(l_r), rtol=10 * tol)
+    for x, y in ((sc.grad, rs.grad), (tc.grad, rt.grad)):
+        assert _rel_l2(x.cpu(), y) <= (2e-2 if precision == "bf16" else 2e-3), _rel_l2(x.cpu(), y)
+
+
 # ---------------------------------------------------------------- C5
 def _c5_setup():
     H, Nc, Nf = 256, 128, 128

@@ -41,7 +41,7 @@ def main():
     only = set(a.only.split(","))
     from codenerf_amd.model import CodeNeRF
     from codenerf_amd.trainer_core import TrainCore
-    from bench import make_pose
+    from bench import make_pose, FLOP_PER_SAMPLE, DW_FOLD_FLOP, DW_BYTES_PER_SAMPLE
 
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
@@ -78,19 +78,20 @@ def main():
                                        act_row0=0, sigma=buf["sig"][:eng.pad(Mc)], rgb=buf["rgb"][:eng.pad(Mc)]),
                    a.reps)
         out["fwd_ms"] = round(t, 4)
-        out["fwd_tflops"] = round(899_328 * Mc / t / 1e9, 1)
+        out["fwd_tflops"] = round(FLOP_PER_SAMPLE["fwd"] * Mc / t / 1e9, 1)
         t = timeit(lambda: eng.mlp_fwd(blob, Mc, rays_o=ro, rays_d=vd, z=z, n_samples=64), a.reps)
         out["fwd_infer_ms"] = round(t, 4)
     if "bwd" in only:
         t = timeit(lambda: eng.mlp_bwd(blob, M, buf["dsig"], buf["drgb"], buf["act"], act_M=cap), a.reps)
         out["bwd_ms"] = round(t, 4)
-        out["bwd_tflops"] = round(853_248 * M / t / 1e9, 1)
+        out["bwd_tflops"] = round(FLOP_PER_SAMPLE["bwd"] * M / t / 1e9, 1)
     if "dw" in only:
         grads = [torch.zeros_like(p) for p in params]
         t = timeit(lambda: eng.mlp_dw(buf["act"], M, zvec, grads, buf["dbuf"], buf["dw"], act_M=cap), a.reps)
         out["dw_ms"] = round(t, 4)
-        out["dw_tflops"] = round(899_328 * M / t / 1e9, 1)
-        out["dw_alg_GBs"] = round(M * 6976 / t / 1e6, 1)     # operand bytes per sample (srncar net, folded)
+        out["dw_tflops"] = round((FLOP_PER_SAMPLE["dw"] * M + DW_FOLD_FLOP) / t / 1e9, 1)
+        es = "fp32" if a.precision == "fp32" else "bf16"
+        out["dw_alg_GBs"] = round(M * DW_BYTES_PER_SAMPLE[es] / t / 1e6, 1)    # operand bytes (srncar net, folded)
         for n in [int(x) for x in a.dw_rows.split(",") if x]:
             n = min(n, M)
             t = timeit(lambda: eng.mlp_dw(buf["act"], n, zvec, grads, buf["dbuf"], buf["dw"], act_M=cap), a.reps)
@@ -107,6 +108,7 @@ def main():
         t = timeit(lambda: torch.sum(xf, dim=0, out=acc), 10)
         out["read_GBs"] = round(x.numel() / t / 1e6, 1)
     out["lib"] = os.environ.get("CODENERF_LIB", "default")
+    out["precision"] = a.precision
     print(json.dumps(out))
 
 
