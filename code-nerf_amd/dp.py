@@ -66,7 +66,9 @@ class GradExchange:
         for t in self.tables:
             t.grad = torch.zeros_like(t)
         self.dist, self.group = dist, group
-        self.clean = True        # every gradient is known to be 0 (zero() is then a no-op)
+        # set by a fused AdamW step that left every gradient at 0: the next
+        # zero() then needs no launch (and consumes the flag)
+        self.clean = False
 
     @property
     def active(self):
@@ -74,11 +76,11 @@ class GradExchange:
 
     def zero(self):
         if self.clean:
+            self.clean = False
             return
         self.bucket.zero()
         for t in self.tables:
             t.grad.zero_()
-        self.clean = True
 
     def mark_dirty(self):
         """A backward wrote into the gradients: the next zero() must clear them."""
