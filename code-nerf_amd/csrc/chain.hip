@@ -173,7 +173,16 @@ struct Chain {
 #ifndef CN_CHAIN_DB
 #define CN_CHAIN_DB 2
 #endif
-  static constexpr int D = BWD ? CN_CHAIN_DB : CN_CHAIN_DF;   // chunks in flight ahead of compute
+#ifndef CN_CHAIN_D3F
+#define CN_CHAIN_D3F 6
+#endif
+#ifndef CN_CHAIN_D3B
+#define CN_CHAIN_D3B 6
+#endif
+  // chunks in flight ahead of compute.  bf16x3 runs one wave per SIMD and
+  // consumes a 16 KiB chunk in ~24 MFMAs (~0.37 us) against ~1.1 us from
+  // LDS-DMA issue to landing, so it keeps twice as many chunks in flight
+  static constexpr int D = kX3 ? (BWD ? CN_CHAIN_D3B : CN_CHAIN_D3F) : (BWD ? CN_CHAIN_DB : CN_CHAIN_DF);
   static constexpr int NS = D + 1;                 // ring slots
 #ifndef CN_CHAIN_PF
 #define CN_CHAIN_PF 2

@@ -47,12 +47,13 @@ def _data(tmp_path):
     return root
 
 
-def _run(tmp_path, root, prec, iters, init=None, seed=0):
+def _run(tmp_path, root, prec, iters, init=None, seed=0, overlap=True):
     from codenerf_amd.trainer import Trainer
     torch.manual_seed(seed)
     np.random.seed(seed)
-    tr = Trainer(f"r_{prec}_{iters}", 0, hpams=hp_many(root, prec), batch_size=B, check_iter=0,
+    tr = Trainer(f"r_{prec}_{iters}_{int(overlap)}", 0, hpams=hp_many(root, prec), batch_size=B, check_iter=0,
                  exp_root=str(tmp_path / "exps"))
+    tr.step_impl.overlap_dw = overlap
     if init is None:
         init = {"model": {k: v.detach().cpu().clone() for k, v in tr.model.state_dict().items()},
                 "shape": tr.shape_codes.weight.detach().cpu().clone(),
@@ -65,6 +66,7 @@ def _run(tmp_path, root, prec, iters, init=None, seed=0):
     torch.manual_seed(1000 + seed)
     np.random.seed(1000 + seed)
     tr.training(0, iters, 1)
+    _run.last = tr
     return np.array(tr.psnr_log), init
 
 
@@ -91,22 +93,80 @@ def test_many_objects_train_psnr_vs_fp32_replay(tmp_path):
         assert np.abs(r - ref).max() <= 0.05, prec
 
 
+def _epoch_means(r):
+    return r[: len(r) // N_OBJ * N_OBJ].reshape(-1, N_OBJ).mean(1)
+
+
 @pytest.mark.timeout(900)
 def test_many_objects_long_horizon_vs_fp32(tmp_path):
-    """LONG_EPOCHS epochs (the CPU replay would take hours): bf16x3 and bf16
-    against HIP fp32 -- which follows the fp32 replay, previous test -- on
-    the last epoch's mean train PSNR and per step."""
+    """LONG_EPOCHS epochs (the CPU replay would take hours): every precision
+    against HIP fp32 -- which follows the fp32 replay, previous test -- by
+    epoch-mean train PSNR.  Training is chaotic over hundreds of steps (an
+    optimiser re-created per epoch, sign-like first steps): the noise floor is
+    HIP fp32 against ITSELF with a different fp32 summation order (the dW
+    pass run in one range instead of two pipelined ones).  Asserted: bf16x3
+    within 0.05 dB of fp32 for every epoch before that floor passes 0.05 dB
+    (the fp32 replayable horizon); past it, every gap is printed beside the
+    floor."""
     root = _data(tmp_path)
     iters = LONG_EPOCHS * N_OBJ
     runs = {}
     runs["fp32"], init = _run(tmp_path, root, "fp32", iters)
+    runs["fp32_order"], _ = _run(tmp_path, root, "fp32", iters, init, overlap=False)
     for prec in ("bf16", "bf16x3"):
         runs[prec], _ = _run(tmp_path, root, prec, iters, init)
-    last = {k: float(v[-N_OBJ:].mean()) for k, v in runs.items()}
-    d = {k: np.abs(v - runs["fp32"]) for k, v in runs.items()}
-    print(f"\nlast-epoch mean train PSNR {last}; first epoch {runs['fp32'][:N_OBJ].mean():.3f} dB (fp32)")
-    for k in ("bf16", "bf16x3"):
-        print(f"{k}: last-epoch gap {last[k] - last['fp32']:+.4f} dB, per-step max |d| {d[k].max():.4f} dB")
-    assert last["fp32"] > runs["fp32"][:N_OBJ].mean() + 3.0        # the run is learning
-    for k in ("bf16", "bf16x3"):
-        assert abs(last[k] - last["fp32"]) <= 0.05, k
+    em = {k: _epoch_means(v) for k, v in runs.items()}
+    gap = {k: np.abs(v - em["fp32"]) for k, v in em.items()}
+    floor = gap["fp32_order"]
+    horizon = int(np.argmax(floor > 0.05)) if (floor > 0.05).any() else LONG_EPOCHS
+    print(f"\nepoch-mean train PSNR (fp32) {np.round(em['fp32'], 3).tolist()}")
+    for k in ("fp32_order", "bf16", "bf16x3"):
+        print(f"|{k} - fp32| per epoch {np.round(gap[k], 4).tolist()}")
+    print(f"fp32 replayable horizon (summation-order floor <= 0.05 dB): {horizon} of {LONG_EPOCHS} epochs; "
+          f"max gap within it: bf16 {gap['bf16'][:horizon].max():.4f}, bf16x3 {gap['bf16x3'][:horizon].max():.4f} dB; "
+          f"last epoch: floor {floor[-1]:.3f}, bf16 {gap['bf16'][-1]:.3f}, bf16x3 {gap['bf16x3'][-1]:.3f} dB")
+    assert em["fp32"][-1] > em["fp32"][0] + 3.0        # the run is learning
+    assert horizon >= 2
+    assert gap["bf16x3"][:horizon].max() <= 0.05
+
+
+@pytest.mark.timeout(600)
+def test_render_psnr_same_weights_across_precisions(tmp_path):
+    """Train PSNR without the trajectory's chaos: the SAME weights and codes
+    (after a few fp32 epochs) render every object's training views in each
+    precision; the PSNR of each (src/trainer.py:98-101: -10 log10 of the
+    mean chunk MSE) against fp32's.  bf16x3 within 1e-3 dB, bf16 within
+    0.05 dB."""
+    from codenerf_amd.data import SRN, collate_one
+    from codenerf_amd.model import CodeNeRF
+    from codenerf_amd.render import ImageStep
+    from codenerf_amd.utils import get_rays
+    root = _data(tmp_path)
+    tr_psnr, _ = _run(tmp_path, root, "fp32", 4 * N_OBJ)
+    tr = _run.last
+    sd = {k: v.detach().clone() for k, v in tr.model.state_dict().items()}
+    st, tt = tr.shape_codes.weight.detach(), tr.texture_codes.weight.detach()
+    ds = SRN("srn_cars", "cars_train", root, 2, crop_img=False, n_train_views=2)
+    z = torch.linspace(0.8 + 0.5 / N, 1.8 - 0.5 / N, N, device="cuda")
+    psnr = {}
+    for prec in ("fp32", "bf16", "bf16x3"):
+        m = CodeNeRF(3, 1, precision=prec)
+        m.load_state_dict(sd)
+        m = m.cuda()
+        step = ImageStep(m, chunk=B)
+        vals = []
+        for idx in range(len(ds)):
+            focal, Hh, Ww, imgs, poses, _, oi = collate_one(ds[idx])
+            for k in range(imgs.shape[1]):
+                ro, vd = get_rays(int(Hh), int(Ww), focal, poses[0, k])
+                rgb, _ = step.render(ro.cuda(), vd.cuda(), z, st[int(oi)], tt[int(oi)])
+                mse = float(((rgb.cpu() - imgs[0, k].reshape(-1, 3)) ** 2).mean())
+                vals.append(-10 * np.log10(mse))
+        psnr[prec] = np.array(vals)
+    d16 = np.abs(psnr["bf16"] - psnr["fp32"]).max()
+    dx3 = np.abs(psnr["bf16x3"] - psnr["fp32"]).max()
+    print(f"\nrender PSNR of the same weights, {len(psnr['fp32'])} views: fp32 mean {psnr['fp32'].mean():.3f} dB; "
+          f"max |bf16 - fp32| {d16:.5f} dB, max |bf16x3 - fp32| {dx3:.6f} dB")
+    assert psnr["fp32"].mean() > tr_psnr[:N_OBJ].mean()      # trained past init
+    assert dx3 <= 1e-3
+    assert d16 <= 0.05
