@@ -57,6 +57,11 @@ CN_DEV uint32_t resid_bf16x2(float lo, float hi, uint32_t p) {
   const float rh = hi - __builtin_bit_cast(float, p & 0xFFFF0000u);
   return pack_bf16x2(rl, rh);
 }
+// ReLU of one fp32 as a signed-int32 max with 0 (one v_max_i32; fmaxf
+// compiles to a canonicalising max plus the max)
+CN_DEV float relu_f32(float v) {
+  return __builtin_bit_cast(float, __builtin_elementwise_max(__builtin_bit_cast(int, v), 0));
+}
 // ReLU of two packed bf16: signed-int16 max with 0 (negative and -0 -> +0)
 CN_DEV uint32_t relu_bf16x2(uint32_t x) {
   typedef __attribute__((ext_vector_type(2))) short s16x2;
@@ -187,7 +192,25 @@ struct Chain {
 #ifndef CN_CHAIN_PF
 #define CN_CHAIN_PF 2
 #endif
-  static constexpr int kPF = CN_CHAIN_PF;          // bf16 A-fragment prefetch distance (blocks)
+#ifndef CN_CHAIN_PF3
+#define CN_CHAIN_PF3 3
+#endif
+  static constexpr int kPF = kX3 ? CN_CHAIN_PF3 : CN_CHAIN_PF;   // A-fragment prefetch distance (blocks)
+#ifndef CN_CHAIN_ASMLDS3
+#define CN_CHAIN_ASMLDS3 1
+#endif
+#ifndef CN_CHAIN_ASMLDS
+#define CN_CHAIN_ASMLDS 0
+#endif
+  // A fragments by explicit ds_read_b128 + counted lgkmcnt waits.  Left to
+  // itself the compiler's waitcnt pass emits lgkmcnt(0) before every MFMA, so
+  // each MFMA also waits for the prefetch issued just before it (its LDS
+  // latency exposed once per block: with one wave per SIMD, bf16x3, nothing
+  // hides it).  Sound because LDS reads return in order and no scalar load
+  // is in flight inside the MFMA stream (every s_load of these kernels is in
+  // the prologue, before the first barrier -- checked on the ISA); extra
+  // compiler-issued LDS reads only make a counted wait stricter.
+  static constexpr bool kAsmLds = kX3 ? CN_CHAIN_ASMLDS3 : CN_CHAIN_ASMLDS;
 #ifndef CN_CHAIN_SB
 #define CN_CHAIN_SB 1
 #endif
@@ -320,9 +343,20 @@ struct Chain {
       // bf16: A fragments are read kPF blocks ahead of their MFMA (rolling
       // register buffer), so the LDS latency hides behind earlier MFMAs
       bf16x8 Abuf[kPF + 1];
+      constexpr int kLast = ((c + 1) * kChunkBlocks <= S::kBlocks ? kChunkBlocks : S::kBlocks - c * kChunkBlocks) - 1;
+      const uint32_t sbase = lds_addr(slot);
+      auto aread = [&](auto bbc) {
+        constexpr int bb = bbc;
+        u32x4 r;
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(sbase), "n"(bb * kBlockBytes));
+        Abuf[bb % (kPF + 1)] = __builtin_bit_cast(bf16x8, r);
+      };
       if constexpr (kBf16)
         static_for<0, kPF>([&](auto bb) {
-          if constexpr (c * kChunkBlocks + bb < S::kBlocks) Abuf[bb] = *(const bf16x8*)(slot + bb * kBlockBytes);
+          if constexpr (bb <= kLast) {
+            if constexpr (kAsmLds) aread(bb);
+            else Abuf[bb] = *(const bf16x8*)(slot + bb * kBlockBytes);
+          }
         });
       static_for<0, kChunkBlocks>([&](auto bb) {
         constexpr int g = c * kChunkBlocks + bb;
@@ -334,8 +368,14 @@ struct Chain {
           constexpr int part = (lb % S::bpt(li)) % S::kAmul;   // bf16x3: 0 = W_hi, 1 = W_lo fragment
           const char* ap = slot + bb * kBlockBytes;
           if constexpr (kBf16) {
-            if constexpr (bb + kPF < kChunkBlocks && g + kPF < S::kBlocks)
+            if constexpr (kAsmLds) {
+              if constexpr (bb + kPF <= kLast) aread(std::integral_constant<int, bb + kPF>{});
+              // the reads issued after block bb's: bb + 1 .. min(bb + kPF, kLast)
+              constexpr int younger = (bb + kPF <= kLast ? bb + kPF : kLast) - bb;
+              asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(Abuf[bb % (kPF + 1)]) : "n"(younger));
+            } else if constexpr (bb + kPF < kChunkBlocks && g + kPF < S::kBlocks) {
               Abuf[(bb + kPF) % (kPF + 1)] = *(const bf16x8*)(ap + kPF * kBlockBytes);
+            }
             acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
                 Abuf[bb % (kPF + 1)], __builtin_bit_cast(bf16x8, bin[kb]),
                 (BWD && kb == 0 && part == 0) ? f32x16{} : acc[t], 0, 0, 0);
@@ -592,7 +632,7 @@ struct Chain {
           }
           if constexpr (kBf16) {
             if constexpr (kX3 && l.epi == EPI_RELU) {
-              v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+              v0 = relu_f32(v0); v1 = relu_f32(v1); v2 = relu_f32(v2); v3 = relu_f32(v3);
             }
             uint32_t p0 = pack_bf16x2(v0, v1), p1 = pack_bf16x2(v2, v3);
             if constexpr (!kX3 && l.epi == EPI_RELU) { p0 = relu_bf16x2(p0); p1 = relu_bf16x2(p1); }

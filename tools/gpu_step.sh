@@ -1,7 +1,7 @@
 #!/bin/bash
-# One GPU call of the build loop: targeted tests (fail fast), kernel timings
-# (tools/kbench.py) per precision and library variant, optional bench lines,
-# then optionally the full check (tools/gpu_check.sh).
+# One GPU call of the build loop: kernel timings (tools/kbench.py) per
+# precision and library variant, optional bench lines, targeted tests (fail
+# fast), then optionally the full check (tools/gpu_check.sh).
 #   bash tools/gpu_step.sh TAG "pytest targets" [full]
 # env: KB_PRECS (default "bf16 bf16x3"), KB_VARIANTS (library variants
 #      code-nerf_amd/libcodenerf_hip_<v>.so besides the default, e.g. "d4"),
@@ -10,11 +10,6 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out; mkdir -p $O; cd $R
 TAG=$1; TARGETS=$2; FULL=$3
-if [ -n "$TARGETS" ]; then
-  timeout -k 10 1000 python -u -m pytest $TARGETS -x -v -s --timeout 900 --timeout-method thread > $O/pt_$TAG.log 2>&1 \
-    || { echo "targeted tests failed"; grep -E "PASS|FAIL|Error|error|assert" $O/pt_$TAG.log | tail -40; exit 1; }
-  grep -E "passed|failed" $O/pt_$TAG.log | tail -2
-fi
 for p in ${KB_PRECS-bf16 bf16x3}; do
   for v in default $KB_VARIANTS; do
     lib=""; [ "$v" != default ] && lib=$R/code-nerf_amd/libcodenerf_hip_$v.so
@@ -31,4 +26,9 @@ for a in "${BA[@]}"; do
   echo "bench $a: $(tail -1 $O/bench_${TAG}_$i.log | cut -c1-400)"
   i=$((i+1))
 done
+if [ -n "$TARGETS" ]; then
+  timeout -k 10 1000 python -u -m pytest $TARGETS -x -v -s --timeout 900 --timeout-method thread > $O/pt_$TAG.log 2>&1 \
+    || { echo "targeted tests failed"; grep -E "PASS|FAIL|Error|error|assert" $O/pt_$TAG.log | tail -40; exit 1; }
+  grep -E "passed|failed" $O/pt_$TAG.log | tail -2
+fi
 if [ -n "$FULL" ]; then bash tools/gpu_check.sh $TAG || exit 1; fi
