@@ -46,6 +46,11 @@ DW_BYTES_PER_SAMPLE = {"bf16": 6_976, "fp32": 13_952}
 KERNEL_NAMES = {"fwd": "chain_kernel<fwd,train>", "bwd": "chain_kernel<bwd>", "dw": "dw_kernel"}
 
 
+def log(msg):
+    """progress on stderr (a GPU runner kills a command that stays silent)"""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
@@ -73,6 +78,8 @@ def parse():
     ap.add_argument("--no-fp32", action="store_true", help="skip the secondary precisions' figures of the C2 step")
     ap.add_argument("--recompute", action="store_true",
                     help="store-vs-recompute A/B: loss forwards store masks only, a second forward writes the dW planes")
+    ap.add_argument("--cpu-baseline-only", type=int, default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="CPU baseline threads (default: OMP_NUM_THREADS, else all host CPUs)")
     # rehearsal of the N > 1 path on a one-GPU box: gloo, every rank on cuda:0
@@ -237,6 +244,7 @@ def timed_run(wl, steps, warmup, timers, dist, dev):
     for i in range(warmup):
         wl["step"](i)
     torch.cuda.synchronize()
+    log(f"warmup done ({warmup} steps); timing {steps} steps")
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -268,6 +276,10 @@ def main():
         args.H, args.n_coarse, args.n_fine = 128, 64, 0
     elif args.config == "c5":
         args.H, args.n_coarse, args.n_fine, args.precision = 256, 128, 128, "fp32"
+    if args.cpu_baseline_only is not None:
+        # child of cpu_baseline: the CPU oracle only, no device
+        print(json.dumps(_cpu_baseline_at(args.cpu_baseline_only, args, args.cpu_seconds)))
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -284,6 +296,7 @@ def main():
             dist.init_process_group("gloo")
 
     timers = Timers()
+    log(f"config {args.config}, precision {args.precision}, world {world}")
     wl = build_workload(args, dev, rank, world, args.precision, timers, dist)
     dt, median = timed_run(wl, args.steps, args.warmup, timers, dist, dev)
     samples_per_step = wl["samples_per_step"]
@@ -300,6 +313,7 @@ def main():
         del wl
         for prec in [p for p in ("bf16", "bf16x3", "fp32") if p != args.precision]:
             t2 = Timers()
+            log(f"secondary precision {prec}")
             wl2 = build_workload(args, dev, rank, world, prec, t2, dist)
             n2 = max(5, args.steps // (5 if prec == "fp32" else 2))
             dt2, med2 = timed_run(wl2, n2, 3, t2, dist, dev)
@@ -447,11 +461,24 @@ def cpu_model():
     return None
 
 
+def cpu_quota():
+    """CPUs the cgroup grants this process (cpu.max quota / period), or None"""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        return None if q == "max" else max(1, int(int(q) / int(p)))
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(threads, args):
     """The oracle sample below at the box's thread counts: the process's
-    OMP_NUM_THREADS share (16 on the GPU box), the CPUs it may run on
-    (sched_getaffinity) and every host CPU (os.cpu_count()); ``value`` /
-    ``cores`` are the fastest, every count is listed under ``by_threads``."""
+    OMP_NUM_THREADS share (16 on the GPU box), the cgroup CPU quota, the CPUs
+    it may run on (sched_getaffinity) and every host CPU (os.cpu_count()).
+    Each count runs in a child process with a wall-clock limit, so a count
+    far above the quota (the box: 256 host CPUs, a 16-CPU share) cannot stall
+    the bench; a count that does not finish is listed as such.  ``value`` /
+    ``cores`` are the fastest finished count, every count under ``by_threads``."""
     if threads is not None:
         return _cpu_baseline_at(threads, args, 10.0)
     omp = int(os.environ.get("OMP_NUM_THREADS", "0")) or None
@@ -459,13 +486,39 @@ def cpu_baseline(threads, args):
         aff = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         aff = None
-    counts = sorted({c for c in (omp, aff, os.cpu_count()) if c})
-    runs = [_cpu_baseline_at(c, args, 8.0 if len(counts) > 1 else 10.0) for c in counts]
+    quota = cpu_quota()
+    counts = sorted({c for c in (omp, quota, aff, os.cpu_count()) if c})
+    runs, by = [], {}
+    for c in counts:
+        log(f"cpu baseline, {c} threads (child process, limit 90 s)")
+        r = _cpu_baseline_child(c, args, 8.0 if len(counts) > 1 else 10.0, 90)
+        if r is None:
+            by[c] = "did not finish 2 reps within 90 s"
+        else:
+            runs.append(r)
+            by[c] = r["value"]
+    if not runs:
+        return None
     best = dict(max(runs, key=lambda r: r["value"]))
-    best["by_threads"] = {r["cores"]: r["value"] for r in runs}
+    best["by_threads"] = by
     best["affinity_cpus"] = aff
+    best["cgroup_cpu_quota"] = quota
     best["omp_num_threads"] = omp
     return best
+
+
+def _cpu_baseline_child(threads, args, seconds, limit):
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-only", str(threads),
+           "--config", args.config, "--n-coarse", str(args.n_coarse), "--n-fine", str(args.n_fine),
+           "--objects", str(args.objects), "--cpu-seconds", str(seconds)]
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads), HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+    try:
+        out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=limit)
+    except subprocess.TimeoutExpired:
+        return None
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    return json.loads(lines[-1]) if out.returncode == 0 and lines else None
 
 
 def _cpu_baseline_at(threads, args, seconds):
