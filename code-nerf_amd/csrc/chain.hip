@@ -97,8 +97,9 @@ CN_DEV uint32_t relu_mask_bf16x2(uint32_t p, uint32_t word) {
 // product's rounding error recovered by FMA), whole turns removed exactly by
 // v_fract_f32, then v_sin_f32 / v_cos_f32 (input in turns).  Absolute error
 // ~1e-6 at the largest argument (2^9 |x| ~ 1e3 rad), against the 2^-9
-// relative rounding the bf16 operand applies next; the fp32 parity path keeps
-// the correctly rounded sincosf.
+// relative rounding the bf16 operand applies next (bf16x3's hi + lo pair
+// carries ~2^-17: still above the error); the fp32 parity path keeps the
+// correctly rounded sincosf.
 CN_DEV void sincos_turns(float v, float& s, float& c) {
   constexpr float kHi = 0.15915493667125702f, kLo = 6.4206382432985265e-09f;
   const float t = v * kHi;
@@ -179,16 +180,19 @@ struct Chain {
 #define CN_CHAIN_DB 2
 #endif
 #ifndef CN_CHAIN_D3F
-#define CN_CHAIN_D3F 6
+#define CN_CHAIN_D3F 5
 #endif
 #ifndef CN_CHAIN_D3B
-#define CN_CHAIN_D3B 6
+#define CN_CHAIN_D3B 5
 #endif
   // chunks in flight ahead of compute.  bf16x3 runs one wave per SIMD and
   // consumes a 16 KiB chunk in ~24 MFMAs (~0.37 us) against ~1.1 us from
   // LDS-DMA issue to landing, so it keeps twice as many chunks in flight
   static constexpr int D = kX3 ? (BWD ? CN_CHAIN_D3B : CN_CHAIN_D3F) : (BWD ? CN_CHAIN_DB : CN_CHAIN_DF);
-  static constexpr int NS = D + 1;                 // ring slots
+  // ring slots: chunk c + D is issued at chunk c's wait point, which lies in
+  // chunk c - 1's tail (cross-chunk A-fragment prefetch, below), so it refills
+  // the slot of chunk c - 2 -- the last one every wave has finished with
+  static constexpr int NS = D + 2;
 #ifndef CN_CHAIN_PF
 #define CN_CHAIN_PF 2
 #endif
@@ -270,24 +274,86 @@ struct Chain {
     }
     return plane_of(i) && !defers(i) ? l.T * (kBf16 ? 2 : 4) : 0;
   }
-  static constexpr int stores_in_chunk(int c) {
-    int s = 0;
+  // ---------------- epilogue schedule (see the epilogues below)
+#ifndef CN_CHAIN_DIAG
+#define CN_CHAIN_DIAG 1
+#endif
+  // layers whose epilogue is spread over the next layer's first tile
+  static constexpr bool diag(int i) { return CN_CHAIN_DIAG && kBf16 && i + 1 < NL; }
+  // block after whose MFMA(s) tile t of layer i is converted: tiles 0, 1 at
+  // the layer's last block, tile t >= 2 after k-block 2t - 3 of the next
+  // layer's first tile (two k-blocks before k-block 2t reads bin[2t])
+  static constexpr int conv_block(int i, int t) {
+    return (!diag(i) || t < 2) ? S::last_block(i) : S::first_block(i + 1) + S::kAmul * (2 * t - 2) - 1;
+  }
+  static constexpr int final_block(int i) { return conv_block(i, S::L(i).T - 1); }
+  // the diag layer converting tiles at block g (at most one), its first tile, count
+  static constexpr int conv_layer_at(int g) {
     for (int i = 0; i < NL; ++i)
-      if (S::last_block(i) / kChunkBlocks == c) s += stores_of_layer(i);
-    for (int g = c * kChunkBlocks; g < (c + 1) * kChunkBlocks && g < S::kBlocks; ++g)
-      if (deferred_at(g) >= 0) s += 1;
+      if (diag(i) && g >= S::last_block(i) && g <= final_block(i))
+        for (int t = 0; t < S::L(i).T; ++t)
+          if (conv_block(i, t) == g) return i;
+    return -1;
+  }
+  static constexpr int conv_first_tile(int i, int g) {
+    for (int t = 0; t < S::L(i).T; ++t)
+      if (conv_block(i, t) == g) return t;
+    return 0;
+  }
+  static constexpr int conv_tiles(int i, int g) {
+    int n = 0;
+    for (int t = 0; t < S::L(i).T; ++t) n += conv_block(i, t) == g;
+    return n;
+  }
+  // the forward epilogue's final stores (mask words, sigma / pre-activation)
+  static constexpr int final_stores(int i) {
+    if (BWD) return 0;
+    const Layer l = S::L(i);
+    return (TRAIN && l.mask >= 0 ? 1 : 0) + (l.epi == EPI_SHAPE ? (TRAIN ? 2 : 1) : 0);
+  }
+  // VMEM stores issued right after block g's MFMA (an epilogue, a deferred
+  // plane store).  A diag layer's plane stores are all deferred (defers()),
+  // so its only epilogue stores are the final ones.
+  static constexpr int stores_at_block(int g) {
+    int s = 0;
+    for (int i = 0; i < NL; ++i) {
+      if (!diag(i) && S::last_block(i) == g) s += stores_of_layer(i);
+      if (diag(i) && final_block(i) == g) s += final_stores(i);
+    }
+    if (deferred_at(g) >= 0) s += 1;
+    return s;
+  }
+  static constexpr int stores_between(int b0, int b1) {
+    int s = 0;
+    for (int g = b0; g < b1; ++g) s += stores_at_block(g);
     return s;
   }
   static constexpr int issued(int i) { return i < kChunks ? G : 0; }
-  // Younger VMEM ops that may still be in flight when chunk c must have landed.
+  // A-fragment read-ahead distance in blocks (fp32 reads each block in place)
+  static constexpr int kPFe = kBf16 ? kPF : 0;
+  // Wait point of chunk c: before block wp(c) -- kPFe blocks before the
+  // chunk's first block, so the reads of its first fragments are issued while
+  // the previous chunk's last MFMAs run.  There the wave waits for its own
+  // LDS-DMA of chunk c (counted vmcnt), the workgroup barriers (every wave's
+  // part of chunk c has landed; every wave is past chunk c - 2), and chunk
+  // c + D is issued into chunk c - 2's slot.
+  static constexpr int wp(int c) { return c == 0 ? 0 : c * kChunkBlocks - kPFe; }
+  static constexpr int wait_chunk_at(int g) {
+    for (int c = 0; c < kChunks; ++c)
+      if (wp(c) == g) return c;
+    return -1;
+  }
+  // Younger VMEM ops that may still be in flight at chunk c's wait point:
+  // the LDS-DMAs issued after chunk c's and the stores issued since it.
   static constexpr int vm_wait(int c) {
     int n = 0;
     if (c < D) {
-      for (int i = c + 1; i < D; ++i) n += issued(i);
-      for (int i = 0; i < c; ++i) n += issued(i + D) + stores_in_chunk(i);
+      for (int i = c + 1; i < D; ++i) n += issued(i);        // the initial issue, younger than c
+      for (int w = 0; w < c; ++w) n += issued(w + D);        // wait points 0 .. c-1
+      n += stores_between(0, wp(c));
     } else {
-      n += stores_in_chunk(c - D);
-      for (int i = c - D + 1; i < c; ++i) n += issued(i + D) + stores_in_chunk(i);
+      for (int w = c - D + 1; w < c; ++w) n += issued(w + D);
+      n += stores_between(wp(c - D), wp(c));
     }
     return n;
   }
@@ -337,91 +403,107 @@ struct Chain {
     static_for<0, D>([&](auto i) { issue<i>(a, smem, w, lane); });
 
     float sig_part = 0.f;
-    auto chunk = [&](auto cc) {
-      constexpr int c = cc;
-      const char* slot = smem + (c % NS) * kChunkBytes + lane * 16;
-      // bf16: A fragments are read kPF blocks ahead of their MFMA (rolling
-      // register buffer), so the LDS latency hides behind earlier MFMAs
-      bf16x8 Abuf[kPF + 1];
-      constexpr int kLast = ((c + 1) * kChunkBlocks <= S::kBlocks ? kChunkBlocks : S::kBlocks - c * kChunkBlocks) - 1;
-      const uint32_t sbase = lds_addr(slot);
-      auto aread = [&](auto bbc) {
-        constexpr int bb = bbc;
+    MaskAcc mk;
+    // bf16: A fragments are read kPF blocks ahead of their MFMA (rolling
+    // register buffer) across chunk boundaries, so the LDS latency hides
+    // behind earlier MFMAs everywhere, the first blocks of a chunk included
+    bf16x8 Abuf[kPF + 1];
+    const uint32_t lbase = lds_addr(smem) + lane * 16;
+    auto block_off = [](int b) { return (b / kChunkBlocks % NS) * kChunkBytes + (b % kChunkBlocks) * kBlockBytes; };
+    auto aread = [&](auto bbc) {
+      constexpr int b = bbc;
+      constexpr int off = block_off(b);
+      // ds_read offsets are 16-bit: the ring's upper 64 KiB through a second base
+      if constexpr (kAsmLds) {
         u32x4 r;
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(sbase), "n"(bb * kBlockBytes));
-        Abuf[bb % (kPF + 1)] = __builtin_bit_cast(bf16x8, r);
-      };
-      if constexpr (kBf16)
-        static_for<0, kPF>([&](auto bb) {
-          if constexpr (bb <= kLast) {
-            if constexpr (kAsmLds) aread(bb);
-            else Abuf[bb] = *(const bf16x8*)(slot + bb * kBlockBytes);
-          }
-        });
-      static_for<0, kChunkBlocks>([&](auto bb) {
-        constexpr int g = c * kChunkBlocks + bb;
-        if constexpr (g < S::kBlocks) {
-          constexpr int li = S::layer_of(g);
-          constexpr int lb = g - S::first_block(li);
-          constexpr int t = lb / S::bpt(li);
-          constexpr int kb = (lb % S::bpt(li)) / S::kAmul;     // MFMA k-block
-          constexpr int part = (lb % S::bpt(li)) % S::kAmul;   // bf16x3: 0 = W_hi, 1 = W_lo fragment
-          const char* ap = slot + bb * kBlockBytes;
-          if constexpr (kBf16) {
-            if constexpr (kAsmLds) {
-              if constexpr (bb + kPF <= kLast) aread(std::integral_constant<int, bb + kPF>{});
-              // the reads issued after block bb's: bb + 1 .. min(bb + kPF, kLast)
-              constexpr int younger = (bb + kPF <= kLast ? bb + kPF : kLast) - bb;
-              asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(Abuf[bb % (kPF + 1)]) : "n"(younger));
-            } else if constexpr (bb + kPF < kChunkBlocks && g + kPF < S::kBlocks) {
-              Abuf[(bb + kPF) % (kPF + 1)] = *(const bf16x8*)(ap + kPF * kBlockBytes);
-            }
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                Abuf[bb % (kPF + 1)], __builtin_bit_cast(bf16x8, bin[kb]),
-                (BWD && kb == 0 && part == 0) ? f32x16{} : acc[t], 0, 0, 0);
-            // bf16x3: W_hi x_lo after W_hi x_hi (same A fragment); the W_lo
-            // fragment (part 1) multiplies x_hi only
-            if constexpr (kX3 && part == 0)
-              acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Abuf[bb % (kPF + 1)],
-                                                               __builtin_bit_cast(bf16x8, binl[kb]), acc[t], 0, 0, 0);
-#if CN_CHAIN_SB
-            // pin the (A-fragment read, MFMA) order: left alone, the machine
-            // scheduler sinks each LDS read next to its MFMA (2 buffers, a
-            // lgkmcnt(0) every other MFMA), exposing the LDS latency kPF hides
-            __builtin_amdgcn_sched_barrier(CN_CHAIN_SB_MASK);
-#endif
-          } else {
-            const f32x4 A = *(const f32x4*)ap;
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[0], bin[4 * kb + 0], (BWD && kb == 0) ? f32x16{} : acc[t],
-                                                          0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[1], bin[4 * kb + 1], acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[2], bin[4 * kb + 2], acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[3], bin[4 * kb + 3], acc[t], 0, 0, 0);
-          }
-          if constexpr (g == S::last_block(li)) {
-            if constexpr (!BWD)
-              epilogue_fwd<li>(a, bin, binl, acc, prm, smem, h, lane, w, m, wglob, voff, sig_part);
-            else
-              epilogue_bwd<li>(a, bin, binl, acc, prm, smem, h, lane, w, m, wglob, voff, ds);
-          }
-          if constexpr (deferred_at(g) >= 0) {
-            constexpr int j = deferred_at(g);
-            constexpr int pl = li - 1;                 // layer whose output bin holds
-            constexpr int plane = S::L(pl).plane;
-            constexpr int F = BWD ? N::dplane_width(plane) : N::plane_width(plane);
-            const u32x4 b = bin[j];                    // tile j / 2, pair j % 2
-            plane_store_pair(slab_rsrc<E>(BWD ? a.dA[plane] : a.Y[plane], F, wglob), voff[4 + (j & 1)], j >> 1,
-                             u32x2{b[0], b[1]}, u32x2{b[2], b[3]});
-          }
-        }
-      });
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(lbase + (off & ~0xFFFF)), "n"(off & 0xFFFF));
+        Abuf[b % (kPF + 1)] = __builtin_bit_cast(bf16x8, r);
+      } else {
+        Abuf[b % (kPF + 1)] = *(const bf16x8*)(smem + off + lane * 16);
+      }
     };
-    static_for<0, kChunks>([&](auto kk) {
-      constexpr int k = kk;
-      wait_vmcnt<vm_wait(k)>();
-      block_barrier();
-      if constexpr (k + D < kChunks) issue<k + D>(a, smem, w, lane);
-      chunk(std::integral_constant<int, k>{});
+    auto block = [&](auto gc) {
+      constexpr int g = gc;
+      constexpr int wc = wait_chunk_at(g);
+      if constexpr (wc >= 0) {
+        wait_vmcnt<vm_wait(wc)>();
+        block_barrier_noread();
+        if constexpr (wc + D < kChunks) issue<wc + D>(a, smem, w, lane);
+        if constexpr (wc == 0 && kBf16)
+          static_for<0, kPF>([&](auto bb) {
+            if constexpr (bb < S::kBlocks) aread(bb);
+          });
+      }
+      constexpr int li = S::layer_of(g);
+      constexpr int lb = g - S::first_block(li);
+      constexpr int t = lb / S::bpt(li);
+      constexpr int kb = (lb % S::bpt(li)) / S::kAmul;     // MFMA k-block
+      constexpr int part = (lb % S::bpt(li)) % S::kAmul;   // bf16x3: 0 = W_hi, 1 = W_lo fragment
+      if constexpr (kBf16) {
+        if constexpr (g + kPF < S::kBlocks) aread(std::integral_constant<int, g + kPF>{});
+        if constexpr (kAsmLds) {
+          // the reads issued after block g's: g + 1 .. min(g + kPF, last)
+          constexpr int younger = (g + kPF < S::kBlocks ? g + kPF : S::kBlocks - 1) - g;
+          asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(Abuf[g % (kPF + 1)]) : "n"(younger));
+        }
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+            Abuf[g % (kPF + 1)], __builtin_bit_cast(bf16x8, bin[kb]),
+            (BWD && kb == 0 && part == 0) ? f32x16{} : acc[t], 0, 0, 0);
+        // bf16x3: W_hi x_lo after W_hi x_hi (same A fragment); the W_lo
+        // fragment (part 1) multiplies x_hi only
+        if constexpr (kX3 && part == 0)
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Abuf[g % (kPF + 1)],
+                                                           __builtin_bit_cast(bf16x8, binl[kb]), acc[t], 0, 0, 0);
+#if CN_CHAIN_SB
+        // pin the (A-fragment read, MFMA) order: left alone, the machine
+        // scheduler sinks each LDS read next to its MFMA (2 buffers, a
+        // lgkmcnt(0) every other MFMA), exposing the LDS latency kPF hides
+        __builtin_amdgcn_sched_barrier(CN_CHAIN_SB_MASK);
+#endif
+      } else {
+        const f32x4 A = *(const f32x4*)(smem + block_off(g) + lane * 16);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[0], bin[4 * kb + 0], (BWD && kb == 0) ? f32x16{} : acc[t],
+                                                      0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[1], bin[4 * kb + 1], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[2], bin[4 * kb + 2], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[3], bin[4 * kb + 3], acc[t], 0, 0, 0);
+      }
+      if constexpr (!diag(li) && g == S::last_block(li)) {
+        if constexpr (!BWD)
+          epilogue_fwd<li>(a, bin, binl, acc, prm, smem, h, lane, w, m, wglob, voff, sig_part, mk);
+        else
+          epilogue_bwd<li>(a, bin, binl, acc, prm, smem, h, lane, w, m, wglob, voff, ds);
+      }
+      constexpr int ci = conv_layer_at(g);       // diagonal schedule: this block's tile conversions
+      if constexpr (ci >= 0) {
+        constexpr int t0 = conv_first_tile(ci, g);
+        static_for<0, conv_tiles(ci, g)>([&](auto k) {
+          constexpr int tt = t0 + k;
+          if constexpr (!BWD)
+            epi_tile_fwd<ci, tt>(a, bin, binl, acc, prm, h, wglob, voff, sig_part, mk);
+          else
+            epi_tile_bwd<ci, tt>(a, bin, binl, acc, prm, smem, h, lane, w, wglob, voff, ds);
+        });
+        if constexpr (!BWD && g == final_block(ci))
+          epi_final_fwd<ci>(a, bin, binl, prm, smem, lane, w, m, wglob, sig_part, mk);
+      }
+      if constexpr (deferred_at(g) >= 0) {
+        constexpr int j = deferred_at(g);
+        constexpr int pl = li - 1;                 // layer whose output bin holds
+        constexpr int plane = S::L(pl).plane;
+        constexpr int F = BWD ? N::dplane_width(plane) : N::plane_width(plane);
+        const u32x4 b = bin[j];                    // tile j / 2, pair j % 2
+        plane_store_pair(slab_rsrc<E>(BWD ? a.dA[plane] : a.Y[plane], F, wglob), voff[4 + (j & 1)], j >> 1,
+                         u32x2{b[0], b[1]}, u32x2{b[2], b[3]});
+      }
+    };
+    // (two nested loops: one static_for over ~300 blocks would exceed the
+    // template instantiation depth)
+    static_for<0, kChunks>([&](auto cc) {
+      static_for<0, kChunkBlocks>([&](auto bb) {
+        constexpr int g = cc * kChunkBlocks + bb;
+        if constexpr (g < S::kBlocks) block(std::integral_constant<int, g>{});
+      });
     });
   }
 
@@ -430,28 +512,39 @@ struct Chain {
     // (non-issuing waves have no LDS-DMA to wait for: their counted vmcnt
     // waits, sized for G DMAs per chunk, only relax towards their own stores)
     if (kIssuers < WAVES && w >= kIssuers) return;
-    const char* src = (const char*)a.wpack + (size_t)C * kChunkBytes + w * G * kBlockBytes + lane * 16;
+#ifdef CN_CHAIN_NODMA
+    return;    // measurement only: the weight stream's cost (MFMAs read stale LDS)
+#endif
+    // buffer_load ... lds: the per-lane part of the source address is one
+    // fixed VGPR, the chunk / block part a compile-time scalar offset, so an
+    // issue costs no VALU (a global_load_lds needs a 64-bit VGPR address
+    // add per instruction: ~450 VALU per bf16x3 forward wave)
+    const auto rs = mkrsrc(a.wpack);
+    const uint32_t voffs = (uint32_t)(w * G * kBlockBytes + lane * 16);
     char* dst = smem + (C % NS) * kChunkBytes + w * G * kBlockBytes;
 #pragma unroll
     for (int k = 0; k < G; ++k)
-      glds16(src + k * kBlockBytes, (lds_void*)(dst + k * kBlockBytes));
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + k * kBlockBytes), 16, voffs,
+                                               C * kChunkBytes + k * kBlockBytes, 0, 0);
   }
 
-  // accumulators <- bias of forward layer LI (rows 32t + 8g + 4h + i)
+  // accumulator tile t <- bias of forward layer LI (rows 32t + 8g + 4h + i)
   template <int LI>
-  __device__ static void load_bias(f32x16* acc, const float* prm, int h) {
-    constexpr int T = S::L(LI).T;
+  __device__ static void load_bias_tile(f32x16& acc, const float* prm, int h, int t) {
     const float* b = prm + LI * 256 + 4 * h;
 #pragma unroll
-    for (int t = 0; t < T; ++t)
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 v = *(const f32x4*)(b + 32 * t + 8 * g);
+      acc[4 * g + 0] = v[0];
+      acc[4 * g + 1] = v[1];
+      acc[4 * g + 2] = v[2];
+      acc[4 * g + 3] = v[3];
+    }
+  }
+  template <int LI>
+  __device__ static void load_bias(f32x16* acc, const float* prm, int h) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x4 v = *(const f32x4*)(b + 32 * t + 8 * g);
-        acc[t][4 * g + 0] = v[0];
-        acc[t][4 * g + 1] = v[1];
-        acc[t][4 * g + 2] = v[2];
-        acc[t][4 * g + 3] = v[3];
-      }
+    for (int t = 0; t < S::L(LI).T; ++t) load_bias_tile<LI>(acc[t], prm, h, t);
   }
 
   // ---------------- prologues
@@ -480,7 +573,7 @@ struct Chain {
       const int comp = p % 3, oct = p / 3;
       const float v = (comp == 0 ? x[0] : comp == 1 ? x[1] : x[2]) * (float)(1 << oct);
       float sn, cs;
-      if constexpr (kBf16 && !kX3 && CN_PE_HW) sincos_turns(v, sn, cs);
+      if constexpr (kBf16 && CN_PE_HW) sincos_turns(v, sn, cs);
       else sincosf(v, &sn, &cs);
       pe[2 + 2 * k] = sn;
       pe[3 + 2 * k] = cs;
@@ -494,7 +587,7 @@ struct Chain {
       if (p >= 0) {
         const int comp = p % 3, oct = p / 3;
         const float v = (comp == 0 ? d[0] : comp == 1 ? d[1] : d[2]) * (float)(1 << oct);
-        if constexpr (kBf16 && !kX3 && CN_PE_HW) sincos_turns(v, sn, cs);
+        if constexpr (kBf16 && CN_PE_HW) sincos_turns(v, sn, cs);
         else sincosf(v, &sn, &cs);
       }
       dp[2 + 2 * k] = sn;
@@ -592,10 +685,126 @@ struct Chain {
   }
 
   // ---------------- epilogues
+  // A layer's epilogue is split per output tile (epi_tile_*) plus a final
+  // part (epi_final_fwd: mask words, sigma head, dir operand).  Run whole at
+  // the layer's last block (fp32, the last layers), or -- bf16 -- spread over
+  // the NEXT layer's first output tile ("diagonal" schedule, conv_block):
+  // that tile's k-block 2u needs only bin[2u] / bin[2u + 1], i.e. this
+  // layer's tile u, so tile u is converted two k-blocks ahead of its first
+  // use and the epilogue's VALU work issues between the MFMAs of the next
+  // layer instead of as a burst with the matrix core idle (one wave per
+  // SIMD in bf16x3: nothing else would fill it).
+  struct MaskAcc {
+    uint32_t lo[4], hi[4];
+  };
+  template <int LI, int TT>
+  __device__ static void epi_tile_fwd(const ChainArgs& a, BinT* bin, BinT* binl, f32x16* acc, const float* prm,
+                                      int h, int wglob, const uint32_t* voff, float& sig_part, MaskAcc& mk) {
+    constexpr Layer l = S::L(LI);
+    constexpr int t = TT;
+    if constexpr (t == 0)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) mk.lo[k] = mk.hi[k] = 0u;
+    constexpr int yp = l.plane >= 0 ? l.plane : 0;
+    constexpr int YF = N::plane_width(yp);
+    const auto ry = slab_rsrc<E>(a.Y[yp], YF, wglob);
+    const float* ws = prm + kWsOff + 4 * h;
+    u32x2 pg[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float v0 = acc[t][4 * g + 0], v1 = acc[t][4 * g + 1];
+      float v2 = acc[t][4 * g + 2], v3 = acc[t][4 * g + 3];
+      if constexpr (TRAIN && l.mask >= 0) {
+        // elements 0 / 2 into the low half, 1 / 3 into the high half
+        // (mask_bit): push order q = 8 (t & 1) + 2 g + i / 2
+        mk.lo[t >> 1] = push_sign(push_sign(mk.lo[t >> 1], v0), v2);
+        mk.hi[t >> 1] = push_sign(push_sign(mk.hi[t >> 1], v1), v3);
+      }
+      if constexpr (l.epi == EPI_SHAPE) {
+        const f32x4 w4 = *(const f32x4*)(ws + 32 * t + 8 * g);
+        sig_part = __builtin_fmaf(w4[0], v0, sig_part);
+        sig_part = __builtin_fmaf(w4[1], v1, sig_part);
+        sig_part = __builtin_fmaf(w4[2], v2, sig_part);
+        sig_part = __builtin_fmaf(w4[3], v3, sig_part);
+      }
+      if constexpr (kBf16) {
+        if constexpr (kX3 && l.epi == EPI_RELU) {
+          v0 = relu_f32(v0); v1 = relu_f32(v1); v2 = relu_f32(v2); v3 = relu_f32(v3);
+        }
+        uint32_t p0 = pack_bf16x2(v0, v1), p1 = pack_bf16x2(v2, v3);
+        if constexpr (!kX3 && l.epi == EPI_RELU) { p0 = relu_bf16x2(p0); p1 = relu_bf16x2(p1); }
+        BinT& b = bin[2 * t + (g >> 1)];
+        if ((g & 1) == 0) { b[0] = p0; b[1] = p1; } else { b[2] = p0; b[3] = p1; }
+        if constexpr (kX3) {
+          const uint32_t l0 = resid_bf16x2(v0, v1, p0), l1 = resid_bf16x2(v2, v3, p1);
+          BinT& bl = binl[2 * t + (g >> 1)];
+          if ((g & 1) == 0) { bl[0] = l0; bl[1] = l1; } else { bl[2] = l0; bl[3] = l1; }
+        }
+        pg[g] = u32x2{p0, p1};
+        if constexpr (plane_of(LI) && !defers(LI))
+          if (g & 1) plane_store_pair(ry, voff[4 + (g >> 1)], t, pg[g - 1], pg[g]);
+      } else {
+        if constexpr (l.epi == EPI_RELU) {
+          v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+        }
+        bin[16 * t + 4 * g + 0] = v0;
+        bin[16 * t + 4 * g + 1] = v1;
+        bin[16 * t + 4 * g + 2] = v2;
+        bin[16 * t + 4 * g + 3] = v3;
+        if constexpr (plane_of(LI))
+          plane_store<E>(ry, voff, t, g, v0, v1, v2, v3);
+      }
+    }
+    // this tile's accumulator starts the next layer's tile t
+    if constexpr (t < S::L(LI + 1).T) load_bias_tile<LI + 1>(acc[t], prm, h, t);
+  }
+
+  template <int LI>
+  __device__ static void epi_final_fwd(const ChainArgs& a, BinT* bin, BinT* binl, const float* prm,
+                                       const char* smem, int lane, int w, int m, int wglob, float& sig_part,
+                                       MaskAcc& mk) {
+    constexpr Layer l = S::L(LI);
+    if constexpr (TRAIN && l.mask >= 0) {
+      uint32_t mw[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) mw[k] = (mk.hi[k] << 16) | (mk.lo[k] & 0xFFFFu);
+      bstore128(mkrsrc(a.masks + (size_t)wglob * N::kMasks * 256), ((uint32_t)l.mask * 64 + lane) * 16,
+                u32x4{mw[0], mw[1], mw[2], mw[3]});
+    }
+    if constexpr (l.epi == EPI_SHAPE) {
+      const float tot = sig_part + __shfl_xor(sig_part, 32);
+      const float pre = tot + prm[kMiscOff];
+      // both lane halves hold the full sum: every lane stores (same value,
+      // same address), so the store count per wave is fixed for vmcnt
+      bstore32(mkrsrc(a.sigma), (uint32_t)m * 4, f2u(softplus20(pre)));
+      if constexpr (TRAIN) bstore32(mkrsrc(a.spre), (uint32_t)m * 4, f2u(pre));
+    }
+    // the next layer (viewdir) takes the dir operand from the LDS stash
+    if constexpr (S::L(LI + 1).in_kind == IN_ACC_DIR) {
+      const char* stash = smem + kDirOff + (w * 64 + lane) * kDirStash;
+      if constexpr (kBf16) {
+        bin[16] = ((const u32x4*)stash)[0];
+        bin[17] = ((const u32x4*)stash)[1];
+        if constexpr (kX3) {
+          binl[16] = ((const u32x4*)stash)[2];
+          binl[17] = ((const u32x4*)stash)[3];
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x4 v = ((const f32x4*)stash)[q];
+          bin[128 + 4 * q + 0] = v[0]; bin[128 + 4 * q + 1] = v[1];
+          bin[128 + 4 * q + 2] = v[2]; bin[128 + 4 * q + 3] = v[3];
+        }
+      }
+    }
+  }
+
+  // the whole forward epilogue at the layer's last block
   template <int LI>
   __device__ static void epilogue_fwd(const ChainArgs& a, BinT* bin, BinT* binl, f32x16* acc, const float* prm,
                                       const char* smem, int h, int lane, int w, int m, int wglob,
-                                      const uint32_t* voff, float& sig_part) {
+                                      const uint32_t* voff, float& sig_part, MaskAcc& mk) {
     constexpr Layer l = S::L(LI);
     if constexpr (l.epi == EPI_RGB) {
       if (h == 0) {
@@ -603,97 +812,9 @@ struct Chain {
         a.rgb[3 * m + 1] = acc[0][1];
         a.rgb[3 * m + 2] = acc[0][2];
       }
-      return;
     } else {
-      uint32_t mlo[4] = {0u, 0u, 0u, 0u}, mhi[4] = {0u, 0u, 0u, 0u};
-      constexpr int yp = l.plane >= 0 ? l.plane : 0;
-      constexpr int YF = N::plane_width(yp);
-      const auto ry = slab_rsrc<E>(a.Y[yp], YF, wglob);
-      const float* ws = prm + kWsOff + 4 * h;
-#pragma unroll
-      for (int t = 0; t < l.T; ++t) {
-        u32x2 pg[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          float v0 = acc[t][4 * g + 0], v1 = acc[t][4 * g + 1];
-          float v2 = acc[t][4 * g + 2], v3 = acc[t][4 * g + 3];
-          if constexpr (TRAIN && l.mask >= 0) {
-            // elements 0 / 2 into the low half, 1 / 3 into the high half
-            // (mask_bit): push order q = 8 (t & 1) + 2 g + i / 2
-            mlo[t >> 1] = push_sign(push_sign(mlo[t >> 1], v0), v2);
-            mhi[t >> 1] = push_sign(push_sign(mhi[t >> 1], v1), v3);
-          }
-          if constexpr (l.epi == EPI_SHAPE) {
-            const f32x4 w4 = *(const f32x4*)(ws + 32 * t + 8 * g);
-            sig_part = __builtin_fmaf(w4[0], v0, sig_part);
-            sig_part = __builtin_fmaf(w4[1], v1, sig_part);
-            sig_part = __builtin_fmaf(w4[2], v2, sig_part);
-            sig_part = __builtin_fmaf(w4[3], v3, sig_part);
-          }
-          if constexpr (kBf16) {
-            if constexpr (kX3 && l.epi == EPI_RELU) {
-              v0 = relu_f32(v0); v1 = relu_f32(v1); v2 = relu_f32(v2); v3 = relu_f32(v3);
-            }
-            uint32_t p0 = pack_bf16x2(v0, v1), p1 = pack_bf16x2(v2, v3);
-            if constexpr (!kX3 && l.epi == EPI_RELU) { p0 = relu_bf16x2(p0); p1 = relu_bf16x2(p1); }
-            BinT& b = bin[2 * t + (g >> 1)];
-            if ((g & 1) == 0) { b[0] = p0; b[1] = p1; } else { b[2] = p0; b[3] = p1; }
-            if constexpr (kX3) {
-              const uint32_t l0 = resid_bf16x2(v0, v1, p0), l1 = resid_bf16x2(v2, v3, p1);
-              BinT& bl = binl[2 * t + (g >> 1)];
-              if ((g & 1) == 0) { bl[0] = l0; bl[1] = l1; } else { bl[2] = l0; bl[3] = l1; }
-            }
-            pg[g] = u32x2{p0, p1};
-            if constexpr (plane_of(LI) && !defers(LI))
-              if (g & 1) plane_store_pair(ry, voff[4 + (g >> 1)], t, pg[g - 1], pg[g]);
-          } else {
-            if constexpr (l.epi == EPI_RELU) {
-              v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
-            }
-            bin[16 * t + 4 * g + 0] = v0;
-            bin[16 * t + 4 * g + 1] = v1;
-            bin[16 * t + 4 * g + 2] = v2;
-            bin[16 * t + 4 * g + 3] = v3;
-            if constexpr (plane_of(LI))
-              plane_store<E>(ry, voff, t, g, v0, v1, v2, v3);
-          }
-        }
-      }
-      if constexpr (TRAIN && l.mask >= 0) {
-        uint32_t mw[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) mw[k] = (mhi[k] << 16) | (mlo[k] & 0xFFFFu);
-        bstore128(mkrsrc(a.masks + (size_t)wglob * N::kMasks * 256), ((uint32_t)l.mask * 64 + lane) * 16,
-                  u32x4{mw[0], mw[1], mw[2], mw[3]});
-      }
-      if constexpr (l.epi == EPI_SHAPE) {
-        const float tot = sig_part + __shfl_xor(sig_part, 32);
-        const float pre = tot + prm[kMiscOff];
-        // both lane halves hold the full sum: every lane stores (same value,
-        // same address), so the store count per wave is fixed for vmcnt
-        bstore32(mkrsrc(a.sigma), (uint32_t)m * 4, f2u(softplus20(pre)));
-        if constexpr (TRAIN) bstore32(mkrsrc(a.spre), (uint32_t)m * 4, f2u(pre));
-      }
-      // the next layer (viewdir) takes the dir operand from the LDS stash
-      if constexpr (S::L(LI + 1).in_kind == IN_ACC_DIR) {
-        const char* stash = smem + kDirOff + (w * 64 + lane) * kDirStash;
-        if constexpr (kBf16) {
-          bin[16] = ((const u32x4*)stash)[0];
-          bin[17] = ((const u32x4*)stash)[1];
-          if constexpr (kX3) {
-            binl[16] = ((const u32x4*)stash)[2];
-            binl[17] = ((const u32x4*)stash)[3];
-          }
-        } else {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const f32x4 v = ((const f32x4*)stash)[q];
-            bin[128 + 4 * q + 0] = v[0]; bin[128 + 4 * q + 1] = v[1];
-            bin[128 + 4 * q + 2] = v[2]; bin[128 + 4 * q + 3] = v[3];
-          }
-        }
-      }
-      load_bias<LI + 1>(acc, prm, h);
+      static_for<0, l.T>([&](auto t) { epi_tile_fwd<LI, t>(a, bin, binl, acc, prm, h, wglob, voff, sig_part, mk); });
+      epi_final_fwd<LI>(a, bin, binl, prm, smem, lane, w, m, wglob, sig_part, mk);
     }
   }
 
@@ -704,67 +825,70 @@ struct Chain {
   static constexpr int mask_q(int t, int g, int i) { return (t & 1) * 8 + 2 * g + (i >> 1); }
   static constexpr int mask_pos(int t, int g, int i) { return ((i & 1) ? 31 : 15) - mask_q(t, g, i); }
 
+  template <int LI, int TT>
+  __device__ static void epi_tile_bwd(const ChainArgs& a, BinT* bin, BinT* binl, f32x16* acc, const float* prm,
+                                      const char* smem, int h, int lane, int w, int wglob, const uint32_t* voff,
+                                      float ds) {
+    constexpr Layer l = S::L(LI);
+    constexpr int t = TT;
+    constexpr int width = N::dplane_width(l.plane);
+    const auto rdA = slab_rsrc<E>(a.dA[l.plane], width, wglob);
+    uint32_t mw = 0u;     // the mask word of this tile pair
+    if constexpr (l.epi == EPI_BMASK)
+      mw = *(const uint32_t*)(smem + kMaskOff + (((size_t)w * N::kMasks + l.mask) * 64 + lane) * 16 + 4 * (t >> 1));
+    const float* ws = prm + kWsOff + 4 * h;
+    u32x2 pg[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[i] = acc[t][4 * g + i];
+        if constexpr (l.epi == EPI_BMASK && !kBf16) v[i] = relu_mask(v[i], mw, mask_pos(t, g, i));
+      }
+      if constexpr (l.epi == EPI_BSIGMA) {
+        const f32x4 w4 = *(const f32x4*)(ws + 32 * t + 8 * g);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = fadd_rn(v[i], fmul_rn(ds, w4[i]));
+      }
+      if constexpr (kBf16) {
+        uint32_t p0 = pack_bf16x2(v[0], v[1]), p1 = pack_bf16x2(v[2], v[3]);
+        uint32_t l0 = 0u, l1 = 0u;
+        if constexpr (kX3) { l0 = resid_bf16x2(v[0], v[1], p0); l1 = resid_bf16x2(v[2], v[3], p1); }
+        if constexpr (l.epi == EPI_BMASK) {
+          static_for<0, 4>([&](auto gg) {
+            if (gg == g) {
+              p0 = relu_mask_bf16x2<mask_q(t & 1, gg, 0)>(p0, mw);
+              p1 = relu_mask_bf16x2<mask_q(t & 1, gg, 2)>(p1, mw);
+              if constexpr (kX3) {
+                l0 = relu_mask_bf16x2<mask_q(t & 1, gg, 0)>(l0, mw);
+                l1 = relu_mask_bf16x2<mask_q(t & 1, gg, 2)>(l1, mw);
+              }
+            }
+          });
+        }
+        BinT& b = bin[2 * t + (g >> 1)];
+        if ((g & 1) == 0) { b[0] = p0; b[1] = p1; } else { b[2] = p0; b[3] = p1; }
+        if constexpr (kX3) {
+          BinT& bl = binl[2 * t + (g >> 1)];
+          if ((g & 1) == 0) { bl[0] = l0; bl[1] = l1; } else { bl[2] = l0; bl[3] = l1; }
+        }
+        pg[g] = u32x2{p0, p1};
+        if constexpr (plane_of(LI) && !defers(LI))
+          if (g & 1) plane_store_pair(rdA, voff[4 + (g >> 1)], t, pg[g - 1], pg[g]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bin[16 * t + 4 * g + i] = v[i];
+        if constexpr (plane_of(LI)) plane_store<E>(rdA, voff, t, g, v[0], v[1], v[2], v[3]);
+      }
+    }
+  }
+
   template <int LI>
   __device__ static void epilogue_bwd(const ChainArgs& a, BinT* bin, BinT* binl, f32x16* acc, const float* prm,
                                       const char* smem, int h, int lane, int w, int m, int wglob,
                                       const uint32_t* voff, float ds) {
-    constexpr Layer l = S::L(LI);
-    constexpr int width = N::dplane_width(l.plane);
-    const auto rdA = slab_rsrc<E>(a.dA[l.plane], width, wglob);
-    u32x4 mw = u32x4{0u, 0u, 0u, 0u};
-    if constexpr (l.epi == EPI_BMASK)
-      mw = *(const u32x4*)(smem + kMaskOff + (((size_t)w * N::kMasks + l.mask) * 64 + lane) * 16);
-    const float* ws = prm + kWsOff + 4 * h;
-#pragma unroll
-    for (int t = 0; t < l.T; ++t) {
-      u32x2 pg[4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        float v[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          v[i] = acc[t][4 * g + i];
-          if constexpr (l.epi == EPI_BMASK && !kBf16) v[i] = relu_mask(v[i], mw[t >> 1], mask_pos(t, g, i));
-        }
-        if constexpr (l.epi == EPI_BSIGMA) {
-          const f32x4 w4 = *(const f32x4*)(ws + 32 * t + 8 * g);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = fadd_rn(v[i], fmul_rn(ds, w4[i]));
-        }
-        if constexpr (kBf16) {
-          uint32_t p0 = pack_bf16x2(v[0], v[1]), p1 = pack_bf16x2(v[2], v[3]);
-          uint32_t l0 = 0u, l1 = 0u;
-          if constexpr (kX3) { l0 = resid_bf16x2(v[0], v[1], p0); l1 = resid_bf16x2(v[2], v[3], p1); }
-          if constexpr (l.epi == EPI_BMASK) {
-            static_for<0, 2>([&](auto gi) {
-              static_for<0, 4>([&](auto gg) {
-                if (gg == g && gi == (t & 1)) {
-                  p0 = relu_mask_bf16x2<mask_q(gi, gg, 0)>(p0, mw[t >> 1]);
-                  p1 = relu_mask_bf16x2<mask_q(gi, gg, 2)>(p1, mw[t >> 1]);
-                  if constexpr (kX3) {
-                    l0 = relu_mask_bf16x2<mask_q(gi, gg, 0)>(l0, mw[t >> 1]);
-                    l1 = relu_mask_bf16x2<mask_q(gi, gg, 2)>(l1, mw[t >> 1]);
-                  }
-                }
-              });
-            });
-          }
-          BinT& b = bin[2 * t + (g >> 1)];
-          if ((g & 1) == 0) { b[0] = p0; b[1] = p1; } else { b[2] = p0; b[3] = p1; }
-          if constexpr (kX3) {
-            BinT& bl = binl[2 * t + (g >> 1)];
-            if ((g & 1) == 0) { bl[0] = l0; bl[1] = l1; } else { bl[2] = l0; bl[3] = l1; }
-          }
-          pg[g] = u32x2{p0, p1};
-          if constexpr (plane_of(LI) && !defers(LI))
-            if (g & 1) plane_store_pair(rdA, voff[4 + (g >> 1)], t, pg[g - 1], pg[g]);
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) bin[16 * t + 4 * g + i] = v[i];
-          if constexpr (plane_of(LI)) plane_store<E>(rdA, voff, t, g, v[0], v[1], v[2], v[3]);
-        }
-      }
-    }
+    static_for<0, S::L(LI).T>([&](auto t) { epi_tile_bwd<LI, t>(a, bin, binl, acc, prm, smem, h, lane, w, wglob, voff, ds); });
   }
 };
 

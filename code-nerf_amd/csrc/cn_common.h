@@ -73,6 +73,16 @@ CN_DEV void block_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// The same barrier without the lgkmcnt(0): for a ring whose refilled slot no
+// wave can still be reading (the chain kernels refill chunk c - 2's slot, whose
+// fragments every wave has already fed to its MFMAs), so the reads in flight
+// ahead of the barrier keep hiding their latency behind it.
+CN_DEV void block_barrier_noread() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 CN_DEV float bf2f(__bf16 x) { return (float)x; }
 
 // Softplus(beta=1, threshold=20) as torch.nn.Softplus.
