@@ -92,6 +92,9 @@ def positional_encoding(x, n_freq):
 # emulation probes (tools/split_emu.py): keys fw_w, fw_x (forward), bw_w,
 # bw_dy (dX), dw_x, dw_dy (dW); values "b" (bf16), "s" (hi + lo), "f" (fp32).
 _OPS_BF16 = dict(fw_w="b", fw_x="b", bw_w="b", bw_dy="b", dw_x="b", dw_dy="b")
+# the bf16x3 kernels (chain.hip): weights and layer inputs split in the
+# forward, weights and upstream gradients split in dX, the dW operands bf16
+OPS_BF16X3 = dict(fw_w="s", fw_x="s", bw_w="s", bw_dy="s", dw_x="b", dw_dy="b")
 _BF16 = {"on": False, "ops": dict(_OPS_BF16)}
 
 
@@ -110,26 +113,26 @@ def _q(t, how):
 
 class _Bf16Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b):
-        o = _BF16["ops"]
+    def forward(ctx, x, w, b, o):
         ctx.save_for_backward(x, w)
+        ctx.o = o
         return _q(x, o["fw_x"]) @ _q(w, o["fw_w"]).t() + b
 
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
-        o = _BF16["ops"]
+        o = ctx.o
         dx = _q(dy, o["bw_dy"]) @ _q(w, o["bw_w"])
         d2 = _q(dy, o["dw_dy"]).reshape(-1, dy.shape[-1])
         x2 = _q(x, o["dw_x"]).reshape(-1, x.shape[-1])
-        return dx, d2.t() @ x2, d2.sum(0)
+        return dx, d2.t() @ x2, d2.sum(0), None
 
 
 class bf16_operands:
     """with ref_cpu.bf16_operands(): ... -- the bf16 kernels' arithmetic;
     ``bf16_operands(split_w=True)`` the compensated bf16x2 kernels'."""
 
-    def __init__(self, split_w=False, split_x=False, split_dy=False, ops=None):
+    def __init__(self, split_w=False, split_x=False, split_dy=False, ops=None, layer_ops=None):
         o = dict(_OPS_BF16)
         if split_w:
             o.update(fw_w="s", bw_w="s")
@@ -138,10 +141,12 @@ class bf16_operands:
         if split_dy:
             o.update(bw_dy="s", dw_dy="s")
         o.update(ops or {})
-        self.cfg = {"on": True, "ops": o}
+        # per-layer overrides (emulation probes): {layer name: {op: how}}
+        lo = {k: dict(o, **v) for k, v in (layer_ops or {}).items()}
+        self.cfg = {"on": True, "ops": o, "layer_ops": lo}
 
     def __enter__(self):
-        self.prev = {"on": _BF16["on"], "ops": _BF16["ops"]}
+        self.prev = {"on": _BF16["on"], "ops": _BF16["ops"], "layer_ops": _BF16.get("layer_ops", {})}
         _BF16.update(self.cfg)
 
     def __exit__(self, *exc):
@@ -150,8 +155,18 @@ class bf16_operands:
 
 def _lin(p, name, x):
     if _BF16["on"] and "latent" not in name and not name.startswith("sigma"):
-        return _Bf16Linear.apply(x, p[name + ".weight"], p[name + ".bias"])
+        return _Bf16Linear.apply(x, p[name + ".weight"], p[name + ".bias"],
+                                 _BF16.get("layer_ops", {}).get(name, _BF16["ops"]))
     return F.linear(x, p[name + ".weight"], p[name + ".bias"])
+
+
+def _lin_inj(p, name, h, z):
+    """layer `name` applied to h + z (a latent injection).  In the bf16
+    emulation as the kernels compute it: the injection is folded into the
+    layer's bias in fp32 (latent.hip: b + W z), only h is a bf16 operand."""
+    if _BF16["on"]:
+        return _lin(p, name, h) + F.linear(z, p[name + ".weight"])
+    return _lin(p, name, h + z)
 
 
 def codenerf_forward(p, xyz, viewdir, shape_code, texture_code, shape_blocks=3,
@@ -168,7 +183,7 @@ def codenerf_forward(p, xyz, viewdir, shape_code, texture_code, shape_blocks=3,
         acts["y0"] = h
     for j in range(1, shape_blocks + 1):
         z = F.relu(_lin(p, f"shape_latent_layer_{j}.0", shape_code))
-        h = F.relu(_lin(p, f"shape_layer_{j}.0", h + z))
+        h = F.relu(_lin_inj(p, f"shape_layer_{j}.0", h, z))
         if acts is not None:
             acts[f"y{j}"] = h
     h = _lin(p, "encoding_shape", h)
@@ -181,7 +196,7 @@ def codenerf_forward(p, xyz, viewdir, shape_code, texture_code, shape_blocks=3,
         acts["y_view"] = h
     for j in range(1, texture_blocks + 1):
         z = F.relu(_lin(p, f"texture_latent_layer_{j}.0", texture_code))
-        h = F.relu(_lin(p, f"texture_layer_{j}.0", h + z))
+        h = F.relu(_lin_inj(p, f"texture_layer_{j}.0", h, z))
         if acts is not None:
             acts[f"y_tex{j}"] = h
     h = F.relu(_lin(p, "rgb.0", h))

@@ -23,7 +23,7 @@ from golden_util import TRAIN_CASES, case_params, load, oracle64_image_step
 
 pytestmark = pytest.mark.gpu
 
-X3_OPS = dict(fw_w="s", fw_x="s", bw_w="s", bw_dy="s", dw_x="b", dw_dy="b")
+from oracle.ref_cpu import OPS_BF16X3 as X3_OPS
 X3_RGB_ABS = 1e-4
 X3_GRAD_REL = 2e-2
 
@@ -68,7 +68,7 @@ def _rel(a, b):
 def test_bf16x3_train_step_vs_reference(case):
     g = load(case)
     m3, st3, tt3, l3, rgb3 = _step(g, "bf16x3")
-    _, _, _, _, rgb16 = _step(g, "bf16")
+    m16, _, _, _, rgb16 = _step(g, "bf16")
     e3 = float(np.abs(rgb3 - g["rgb"]).max())
     e16 = float(np.abs(rgb16 - g["rgb"]).max())
     r64 = oracle64_image_step(g)
@@ -76,8 +76,11 @@ def test_bf16x3_train_step_vs_reference(case):
     ex = float(np.abs(rgb3 - rgb_x).max())
     gerr = {k: _rel(p.grad.cpu().numpy(), r64["params"][k].grad.numpy()) for k, p in m3.named_parameters()}
     gerr_x = {k: _rel(p.grad.cpu().numpy(), p_x[k].grad.numpy()) for k, p in m3.named_parameters()}
+    gerr16 = {k: _rel(p.grad.cpu().numpy(), r64["params"][k].grad.numpy()) for k, p in m16.named_parameters()}
+    worst = sorted(gerr, key=gerr.get)[-3:]
     print(f"\n{case}: rgb max|d| vs golden bf16x3 {e3:.2e} (bf16 {e16:.2e}); vs x3 oracle {ex:.2e}; "
-          f"grad rel-L2 vs f64 worst {max(gerr.values()):.2e}, vs x3 oracle worst {max(gerr_x.values()):.2e}")
+          f"grad rel-L2 vs f64 worst {max(gerr.values()):.2e} (bf16 {max(gerr16.values()):.2e}), "
+          f"vs x3 oracle worst {max(gerr_x.values()):.2e}; worst tensors {[(k, round(gerr[k], 5), round(gerr16[k], 5)) for k in worst]}")
     assert e3 <= X3_RGB_ABS and e3 * 20 <= max(e16, 1e-6)
     assert ex <= 2e-5
     np.testing.assert_allclose(l3, g["chunk_losses"], rtol=2e-4)

@@ -365,7 +365,7 @@ def test_c4_full_size_50_views_properties_and_ray_subset(precision):
     p = ref_cpu.param_tensors(params, requires_grad=False)
     rs = torch.tensor(s0, requires_grad=True)
     rt = torch.tensor(t0, requires_grad=True)
-    ops = {} if precision == "bf16" else dict(ops=dict(fw_w="s", fw_x="s", bw_w="s", bw_dy="s"))
+    ops = {} if precision == "bf16" else dict(ops=ref_cpu.OPS_BF16X3)
     with ref_cpu.bf16_operands(**ops):
         l_r, rgb_r = ref_cpu.image_step(p, rs, rt, 0, ro[a:b].cpu(), vd[a:b].cpu(), z.cpu(), gt[a:b].cpu(),
                                         chunk=2048, reg_coef=1e-4)

@@ -39,7 +39,16 @@ VARIANTS = {
     "bw_s3": dict(ops=dict(bw_w=S, bw_dy=S)),                              # dX chain only
     "bw_dy": dict(ops=dict(bw_dy=S)),
     "bw_w": dict(ops=dict(bw_w=S)),
+    # the forward's W split only (x bf16), dX fully split
+    "fwW_bw3": dict(ops=dict(fw_w=S, bw_w=S, bw_dy=S)),
 }
+# per-layer probes: chain_s3 everywhere except one layer in plain bf16
+_LAYERS = ["encoding_xyz.0", "shape_layer_1.0", "shape_layer_2.0", "shape_layer_3.0", "encoding_shape",
+           "encoding_viewdir.0", "texture_layer_1.0", "rgb.0", "rgb.2"]
+for _l in _LAYERS:
+    VARIANTS["s3_but_" + _l.split(".")[0]] = dict(ops=dict(fw_w=S, fw_x=S, bw_w=S, bw_dy=S),
+                                                  layer_ops={_l: dict(fw_w=B, fw_x=B, bw_w=B, bw_dy=B)})
+    VARIANTS["b16_but_" + _l.split(".")[0]] = dict(layer_ops={_l: dict(fw_w=S, fw_x=S, bw_w=S, bw_dy=S)})
 
 
 def main():
