@@ -46,7 +46,7 @@ pytestmark = pytest.mark.gpu
 
 ITERS, EARLY, TAIL = 900, 30, 100
 SEEDS = (0, 2)              # seed 1 plateaus at 18.8 dB in both precisions within ITERS
-BF16_TAIL_DB = 2.5          # bar on |bf16 - fp32| tail gaps: two fp32 orders differ by 0.6 dB here (docstring)
+BF16_TAIL_DB = 1.0          # bar on |bf16 - fp32| tail gaps (measured round 3: 0.748 / 0.063 dB; two fp32 orders: 0.402)
 X3_STEPS, X3_PREFIX_DB = 18, 0.08    # bf16x3 vs the fp32 replay: 0.05 dB over 18 steps, bound over the prefix
 
 

@@ -6,7 +6,7 @@ OUT=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out
 mkdir -p $OUT
 TAG=${1:-run}
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
-timeout -k 10 500 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu_$TAG.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest_gpu_$TAG.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 900 --timeout-method thread > $OUT/pytest_gpu_$TAG.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest_gpu_$TAG.log; exit 1; }
 tail -3 $OUT/pytest_gpu_$TAG.log
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$TAG.log 2>&1 || { echo "smoke failed"; tail -30 $OUT/smoke_$TAG.log; exit 1; }
 tail -2 $OUT/smoke_$TAG.log
