@@ -97,9 +97,10 @@ CN_DEV uint32_t relu_mask_bf16x2(uint32_t p, uint32_t word) {
 // product's rounding error recovered by FMA), whole turns removed exactly by
 // v_fract_f32, then v_sin_f32 / v_cos_f32 (input in turns).  Absolute error
 // ~1e-6 at the largest argument (2^9 |x| ~ 1e3 rad), against the 2^-9
-// relative rounding the bf16 operand applies next (bf16x3's hi + lo pair
-// carries ~2^-17: still above the error); the fp32 parity path keeps the
-// correctly rounded sincosf.
+// relative rounding the bf16 operand applies next; the fp32 parity path and
+// bf16x3 keep the correctly rounded sincosf (with the hardware sincos,
+// bf16x3's one-object training trajectory left the fp32 replay by 0.093 dB
+// at step 19 instead of 0.061 dB by step 26: tests/test_gpu_converge.py).
 CN_DEV void sincos_turns(float v, float& s, float& c) {
   constexpr float kHi = 0.15915493667125702f, kLo = 6.4206382432985265e-09f;
   const float t = v * kHi;
@@ -573,7 +574,7 @@ struct Chain {
       const int comp = p % 3, oct = p / 3;
       const float v = (comp == 0 ? x[0] : comp == 1 ? x[1] : x[2]) * (float)(1 << oct);
       float sn, cs;
-      if constexpr (kBf16 && CN_PE_HW) sincos_turns(v, sn, cs);
+      if constexpr (kBf16 && !kX3 && CN_PE_HW) sincos_turns(v, sn, cs);
       else sincosf(v, &sn, &cs);
       pe[2 + 2 * k] = sn;
       pe[3 + 2 * k] = cs;
@@ -587,7 +588,7 @@ struct Chain {
       if (p >= 0) {
         const int comp = p % 3, oct = p / 3;
         const float v = (comp == 0 ? d[0] : comp == 1 ? d[1] : d[2]) * (float)(1 << oct);
-        if constexpr (kBf16 && CN_PE_HW) sincos_turns(v, sn, cs);
+        if constexpr (kBf16 && !kX3 && CN_PE_HW) sincos_turns(v, sn, cs);
         else sincosf(v, &sn, &cs);
       }
       dp[2 + 2 * k] = sn;

@@ -33,7 +33,7 @@ def short(name, prec):
         kind = "bwd" if m.group(2) == "true" else "fwd"
         return kind if mode == 1 else f"{kind}_codes" if mode == 2 else f"{kind}_infer"
     m = re.search(r"\bdw_kernel<(\d)>", name)
-    if m and int(m.group(1)) == prec:
+    if m and int(m.group(1)) == min(prec, 1):     # bf16x3 stores bf16 planes: the bf16 dW pass
         return "dw"
     return None
 
@@ -56,6 +56,8 @@ def counters(d):
 def main():
     src, tag = sys.argv[1:3]
     config = sys.argv[3] if len(sys.argv) > 3 else "c2"
+    precision = sys.argv[4] if len(sys.argv) > 4 else ("fp32" if config == "c5" else "bf16")
+    pcode = {"fp32": 0, "bf16": 1, "bf16x3": 2}[precision]
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     prof = os.path.join(repo, "profiles")
     os.makedirs(prof, exist_ok=True)
@@ -92,7 +94,7 @@ def main():
         lines.append(f"| `{name[:90]}` | {r['Calls']} | {avg_ns / 1e3:.1f} | {float(r['Percentage']):.2f} | "
                      f"{fmt(hbm and hbm / 1e9, 3)} | {fmt(gbs, 1)} | {fmt(tfl, 4)} | {fmt(pmc_ns and pmc_ns / 1e3, 1)} | "
                      f"{fmt(util, 3)} | {fmt(clk, 2)} |")
-        s = short(name, 0 if config == "c5" else 1)
+        s = short(name, pcode)
         if s and hbm:
             traffic[s] = {"hbm_bytes": int(hbm), "fetch_kib": f, "write_kib": w, "avg_ns": avg_ns,
                           "mfma_util": util, "eff_clock_ghz": clk, "pmc_pass_avg_ns": pmc_ns, "mfma_flop": mops * 512 if mops else None,
@@ -100,7 +102,7 @@ def main():
     open(os.path.join(prof, f"{tag}_kernels.md"), "w").write("\n".join(lines) + "\n")
     path = os.path.join(prof, "pmc_traffic.json")
     allt = json.load(open(path)) if os.path.exists(path) else {}
-    allt[config] = traffic
+    allt[config if precision == "bf16" or config == "c5" else f"{config}_{precision}"] = traffic
     json.dump(allt, open(path, "w"), indent=1)
     print("\n".join(lines[:18]))
 
