@@ -44,6 +44,9 @@ DW_FOLD_FLOP = 2 * 2 * 257 ** 3
 # the forward / dX chains stored (encoding_shape folded).
 DW_BYTES_PER_SAMPLE = {"bf16": 6_976, "fp32": 13_952}
 KERNEL_NAMES = {"fwd": "chain_kernel<fwd,train>", "bwd": "chain_kernel<bwd>", "dw": "dw_kernel"}
+# algorithmic HBM bytes per ray of the fused ray-major step
+# (24 B origin + direction in, 12 B gt, 12 B rgb out)
+ALG_BYTES_PER_RAY = 48
 
 
 def log(msg):
@@ -62,6 +65,9 @@ def parse():
     ap.add_argument("--precision", default="bf16", choices=["bf16", "bf16x3", "fp32"],
                     help="chain arithmetic: bf16 operands | bf16x3 (hi + lo operands, 3 MFMAs per block) | fp32")
     ap.add_argument("--objects", type=int, default=64)
+    ap.add_argument("--weights", default=None,
+                    help="reference-format checkpoint (models.pth: model_params, shape/texture_code_params) to "
+                         "start from instead of random-init weights (tools/make_bench_weights.py); 'none' = random init")
     # other BASELINE configs, measured for DESIGN.md (the driver runs c2):
     #   c4: optimize.py test-time code optimisation, 50 views x 128^2 x 64
     #       samples per step, fwd + dX only (no weight gradients), bf16
@@ -151,6 +157,16 @@ def build_workload(args, dev, rank, world, precision, timers, dist):
     n_obj = args.objects
     shape_codes = torch.nn.Parameter(torch.randn(n_obj, 256, device=dev) / math.sqrt(128))
     texture_codes = torch.nn.Parameter(torch.randn(n_obj, 256, device=dev) / math.sqrt(128))
+    wpath = weights_path(args)
+    if wpath:
+        # trained weights (the reference's checkpoint keys, src/trainer.py:166-170);
+        # the code tables repeat the checkpoint's objects
+        ck = torch.load(wpath, map_location=dev, weights_only=True)
+        model.load_state_dict(ck["model_params"])
+        with torch.no_grad():
+            for tab, key in ((shape_codes, "shape_code_params"), (texture_codes, "texture_code_params")):
+                w = ck[key]["weight"].to(dev)
+                tab.copy_(w[torch.arange(n_obj, device=dev) % w.shape[0]])
     # identical initial weights and codes on every rank
     broadcast_from(list(model.parameters()) + [shape_codes, texture_codes], dist)
 
@@ -236,6 +252,16 @@ def build_workload(args, dev, rank, world, precision, timers, dist):
     views_per_step = n_views if args.config == "c4" else 1
     samples_per_step = R * (args.n_coarse + args.n_fine) * views_per_step
     return dict(step=step, last=last, core=core, R=R, H=H, radius=radius, samples_per_step=samples_per_step)
+
+
+def weights_path(args):
+    """The checkpoint the bench starts from, or None (random init)."""
+    if args.weights is None or args.weights.lower() == "none":
+        return None
+    p = args.weights if os.path.isabs(args.weights) else os.path.join(REPO, args.weights)
+    if not os.path.exists(p):
+        raise FileNotFoundError(p)
+    return p
 
 
 def timed_run(wl, steps, warmup, timers, dist, dev):
@@ -339,7 +365,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
             "data": f"synthetic ({H}x{H} ray-cast ellipsoid object per rank, poses on a radius-{radius} sphere, "
-                    f"random-init weights)",
+                    + (f"trained weights {os.path.relpath(weights_path(args), REPO)})" if weights_path(args)
+                       else "random-init weights)"),
             "config": {"workload": f"{'srnchair' if args.config == 'c3' else 'srncar'}.json net, {H}x{H} image/object/step, {args.n_coarse}+{args.n_fine} "
                                    f"samples/ray, " + {"c4": "50 views, codes-only fwd+dX+AdamW",
                                                        "c4eval": "one held-out view per step, forward-only + MSE"}.get(
@@ -430,6 +457,21 @@ def roofline(args, timers, samples_per_step, ms, overlapped):
         roof["overlap"] = ("dX chain of row range i on the main stream || dW of range i-1 on a side stream; "
                            "per-kernel spans overlap, so their sum exceeds the step")
     peak = FP32_PEAK_TFLOPS if args.precision == "fp32" else BF16_PEAK_TFLOPS
+    # SURVEY.md 8(d)'s algorithmic view of the dominant kernel, beside the
+    # operand-byte / counter-byte view above: its algorithmic FLOPs against
+    # the MFMA peak, and its counted HBM bytes against the step's algorithmic
+    # bytes (24 B ray + 12 B gt + 12 B rgb out per ray, spread over the ray's
+    # samples) for the samples one launch processes
+    alg_tf = d["mfma"]["achieved"] if d["bound"] == "hbm" else d["achieved"]
+    n_per_ray = args.n_coarse + args.n_fine
+    alg_b = ALG_BYTES_PER_RAY / n_per_ray
+    roof["algorithmic"] = {"mfma_achieved": alg_tf, "mfma_peak": peak, "unit": "TFLOP/s",
+                           "mfma_frac": round(alg_tf / peak, 4), "hbm_bytes_per_sample": round(alg_b, 4)}
+    tr = d.get("traffic")
+    if tr:
+        alg_launch = alg_b * d["samples_per_launch"]
+        roof["algorithmic"].update(hbm_bytes_per_launch=round(alg_launch),
+                                   counter_over_algorithmic_bytes=round(tr["hbm_bytes_per_launch"] / alg_launch, 1))
     step_flops = sum(v for k, v in FLOP_PER_SAMPLE.items() if k in passes) * samples_per_step
     roof["step"] = {"achieved": round(step_flops / (ms * 1e-3) / 1e12, 2), "unit": "TFLOP/s",
                     "frac": round(step_flops / (ms * 1e-3) / 1e12 / peak, 4)}

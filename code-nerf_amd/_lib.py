@@ -11,9 +11,12 @@ import os
 import torch
 
 LIB_NAME = "libcodenerf_hip.so"
-# CODENERF_LIB selects another build of the same library (kernel variants
-# built side by side for A/B measurements); it must export the same ABI.
-LIB_PATH = os.environ.get("CODENERF_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+_IN_TREE = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+# CODENERF_LIB selects another build of the same ABI -- a measurement-only
+# kernel variant built from a patched copy of csrc/ (tools/kbench.py A/Bs).
+# Such a build is loaded only when CODENERF_MEASURE=1 is set as well: the
+# product path (tests, smoke, bench) always runs the in-tree library.
+LIB_PATH = os.environ.get("CODENERF_LIB") or _IN_TREE
 
 ABI_VERSION = 2
 CN_FP32 = 0
@@ -82,8 +85,10 @@ def load_library(path=LIB_PATH):
     if not os.path.exists(path):
         raise HipUnavailable(f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
     lib = ctypes.CDLL(path)
-    variant = os.path.abspath(path) != os.path.abspath(os.path.join(os.path.dirname(os.path.abspath(__file__)),
-                                                                    LIB_NAME))
+    variant = os.path.abspath(path) != os.path.abspath(_IN_TREE)
+    if variant and os.environ.get("CODENERF_MEASURE") != "1":
+        raise HipUnavailable(f"{path} is not the in-tree library: a measurement variant loads only with "
+                             "CODENERF_MEASURE=1")
     for name, (res, args) in _SIGS.items():
         fn = getattr(lib, name, None)
         if fn is None:

@@ -110,9 +110,6 @@ CN_DEV void sincos_turns(float v, float& s, float& c) {
   s = __builtin_amdgcn_sinf(u);
   c = __builtin_amdgcn_cosf(u);
 }
-#ifndef CN_PE_HW
-#define CN_PE_HW 1
-#endif
 
 // shift the sign bit of v into the running mask word (one v_alignbit_b32)
 CN_DEV uint32_t push_sign(uint32_t bits, float v) {
@@ -174,39 +171,15 @@ struct Chain {
   // divides a chunk; a 12-wave workgroup lets waves 0-3 issue 4 blocks each)
   static constexpr int kIssuers = kChunkBlocks % WAVES == 0 ? WAVES : 4;
   static constexpr int G = kChunkBlocks / kIssuers;   // LDS-DMA instructions per issuing wave per chunk
-#ifndef CN_CHAIN_DF
-#define CN_CHAIN_DF 3
-#endif
-#ifndef CN_CHAIN_DB
-#define CN_CHAIN_DB 2
-#endif
-#ifndef CN_CHAIN_D3F
-#define CN_CHAIN_D3F 5
-#endif
-#ifndef CN_CHAIN_D3B
-#define CN_CHAIN_D3B 5
-#endif
   // chunks in flight ahead of compute.  bf16x3 runs one wave per SIMD and
   // consumes a 16 KiB chunk in ~24 MFMAs (~0.37 us) against ~1.1 us from
   // LDS-DMA issue to landing, so it keeps twice as many chunks in flight
-  static constexpr int D = kX3 ? (BWD ? CN_CHAIN_D3B : CN_CHAIN_D3F) : (BWD ? CN_CHAIN_DB : CN_CHAIN_DF);
+  static constexpr int D = kX3 ? 5 : (BWD ? 2 : 3);
   // ring slots: chunk c + D is issued at chunk c's wait point, which lies in
   // chunk c - 1's tail (cross-chunk A-fragment prefetch, below), so it refills
   // the slot of chunk c - 2 -- the last one every wave has finished with
   static constexpr int NS = D + 2;
-#ifndef CN_CHAIN_PF
-#define CN_CHAIN_PF 2
-#endif
-#ifndef CN_CHAIN_PF3
-#define CN_CHAIN_PF3 3
-#endif
-  static constexpr int kPF = kX3 ? CN_CHAIN_PF3 : CN_CHAIN_PF;   // A-fragment prefetch distance (blocks)
-#ifndef CN_CHAIN_ASMLDS3
-#define CN_CHAIN_ASMLDS3 1
-#endif
-#ifndef CN_CHAIN_ASMLDS
-#define CN_CHAIN_ASMLDS 0
-#endif
+  static constexpr int kPF = kX3 ? 3 : 2;   // A-fragment prefetch distance (blocks)
   // A fragments by explicit ds_read_b128 + counted lgkmcnt waits.  Left to
   // itself the compiler's waitcnt pass emits lgkmcnt(0) before every MFMA, so
   // each MFMA also waits for the prefetch issued just before it (its LDS
@@ -215,13 +188,12 @@ struct Chain {
   // is in flight inside the MFMA stream (every s_load of these kernels is in
   // the prologue, before the first barrier -- checked on the ISA); extra
   // compiler-issued LDS reads only make a counted wait stricter.
-  static constexpr bool kAsmLds = kX3 ? CN_CHAIN_ASMLDS3 : CN_CHAIN_ASMLDS;
-#ifndef CN_CHAIN_SB
-#define CN_CHAIN_SB 1
-#endif
-#ifndef CN_CHAIN_SB_MASK
-#define CN_CHAIN_SB_MASK 0x6     // VALU and SALU may cross; LDS reads, MFMAs, VMEM stay in program order
-#endif
+  // (bf16, two waves per SIMD: the other wave hides the latency, and the
+  // counted waits measured no gain there)
+  static constexpr bool kAsmLds = kX3;
+  // sched_barrier mask after each block: VALU and SALU may cross; LDS
+  // reads, MFMAs and VMEM stay in program order
+  static constexpr int kSbMask = 0x6;
   static constexpr int kRingBytes = NS * kChunkBytes;
   static constexpr int kBlobFloats = BiasBlob<SB, TB>::kFloats;
   static constexpr int kWsOff = BiasBlob<SB, TB>::kWs;
@@ -276,11 +248,8 @@ struct Chain {
     return plane_of(i) && !defers(i) ? l.T * (kBf16 ? 2 : 4) : 0;
   }
   // ---------------- epilogue schedule (see the epilogues below)
-#ifndef CN_CHAIN_DIAG
-#define CN_CHAIN_DIAG 1
-#endif
   // layers whose epilogue is spread over the next layer's first tile
-  static constexpr bool diag(int i) { return CN_CHAIN_DIAG && kBf16 && i + 1 < NL; }
+  static constexpr bool diag(int i) { return kBf16 && i + 1 < NL; }
   // block after whose MFMA(s) tile t of layer i is converted: tiles 0, 1 at
   // the layer's last block, tile t >= 2 after k-block 2t - 3 of the next
   // layer's first tile (two k-blocks before k-block 2t reads bin[2t])
@@ -455,12 +424,10 @@ struct Chain {
         if constexpr (kX3 && part == 0)
           acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Abuf[g % (kPF + 1)],
                                                            __builtin_bit_cast(bf16x8, binl[kb]), acc[t], 0, 0, 0);
-#if CN_CHAIN_SB
         // pin the (A-fragment read, MFMA) order: left alone, the machine
         // scheduler sinks each LDS read next to its MFMA (2 buffers, a
         // lgkmcnt(0) every other MFMA), exposing the LDS latency kPF hides
-        __builtin_amdgcn_sched_barrier(CN_CHAIN_SB_MASK);
-#endif
+        __builtin_amdgcn_sched_barrier(kSbMask);
       } else {
         const f32x4 A = *(const f32x4*)(smem + block_off(g) + lane * 16);
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[0], bin[4 * kb + 0], (BWD && kb == 0) ? f32x16{} : acc[t],
@@ -513,9 +480,6 @@ struct Chain {
     // (non-issuing waves have no LDS-DMA to wait for: their counted vmcnt
     // waits, sized for G DMAs per chunk, only relax towards their own stores)
     if (kIssuers < WAVES && w >= kIssuers) return;
-#ifdef CN_CHAIN_NODMA
-    return;    // measurement only: the weight stream's cost (MFMAs read stale LDS)
-#endif
     // buffer_load ... lds: the per-lane part of the source address is one
     // fixed VGPR, the chunk / block part a compile-time scalar offset, so an
     // issue costs no VALU (a global_load_lds needs a 64-bit VGPR address
@@ -574,7 +538,7 @@ struct Chain {
       const int comp = p % 3, oct = p / 3;
       const float v = (comp == 0 ? x[0] : comp == 1 ? x[1] : x[2]) * (float)(1 << oct);
       float sn, cs;
-      if constexpr (kBf16 && !kX3 && CN_PE_HW) sincos_turns(v, sn, cs);
+      if constexpr (kBf16 && !kX3) sincos_turns(v, sn, cs);
       else sincosf(v, &sn, &cs);
       pe[2 + 2 * k] = sn;
       pe[3 + 2 * k] = cs;
@@ -588,7 +552,7 @@ struct Chain {
       if (p >= 0) {
         const int comp = p % 3, oct = p / 3;
         const float v = (comp == 0 ? d[0] : comp == 1 ? d[1] : d[2]) * (float)(1 << oct);
-        if constexpr (kBf16 && !kX3 && CN_PE_HW) sincos_turns(v, sn, cs);
+        if constexpr (kBf16 && !kX3) sincos_turns(v, sn, cs);
         else sincosf(v, &sn, &cs);
       }
       dp[2 + 2 * k] = sn;

@@ -278,17 +278,11 @@ int db_setup(char* act, int act_M, int M, float* dbuf, char* ws, DbArgs* db) {
 template <int P, int SB, int TB>
 ChainSet make_chain_set() {
   using N = Net<SB, TB>;
-#ifndef CN_FWD_WAVES
-#define CN_FWD_WAVES 8
-#endif
-#ifndef CN_BWD_WAVES
-#define CN_BWD_WAVES 8
-#endif
   // bf16: 8-wave workgroups (two waves per SIMD, one workgroup per CU) by
   // default; fp32 (bin operand of 144 VGPRs) and bf16x3 (hi + lo operands,
   // 2 x 72 VGPRs, beside 128 accumulator registers): 4 waves, one per SIMD
-  constexpr int WF = P == CN_P_BF16 ? CN_FWD_WAVES : 4;
-  constexpr int WB = P == CN_P_BF16 ? CN_BWD_WAVES : 4;
+  constexpr int WF = P == CN_P_BF16 ? 8 : 4;
+  constexpr int WB = P == CN_P_BF16 ? 8 : 4;
   ChainSet s;
   s.prec = P != CN_P_FP32;     // activation-plane element type: 1 = bf16 (bf16, bf16x3)
   s.x3 = P == CN_P_BF16X3;

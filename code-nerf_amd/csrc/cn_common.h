@@ -129,17 +129,15 @@ CN_DEV __amdgpu_buffer_rsrc_t mkrsrc(const void* p, bool live) {
 // The chain kernels stream GBs of activations that only the NEXT kernel
 // reads; keeping them in the XCD's 4 MiB L2 would evict the weight pack that
 // every workgroup re-reads from it.
-#ifndef CN_STORE_AUX
-#define CN_STORE_AUX 2
-#endif
+constexpr int kStoreAux = 2;
 CN_DEV void bstore32(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t v, int soff = 0) {
-  __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)off, soff, CN_STORE_AUX);
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)off, soff, kStoreAux);
 }
 CN_DEV void bstore64(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x2 v, int soff = 0) {
-  __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)off, soff, CN_STORE_AUX);
+  __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)off, soff, kStoreAux);
 }
 CN_DEV void bstore128(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v, int soff = 0) {
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, soff, CN_STORE_AUX);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, soff, kStoreAux);
 }
 CN_DEV uint32_t f2u(float x) { return __builtin_bit_cast(uint32_t, x); }
 // 4 consecutive plane elements through a buffer descriptor

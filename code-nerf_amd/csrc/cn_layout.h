@@ -23,10 +23,7 @@ constexpr int kDirFreq = 4;
 constexpr int kPeSlots = 64;   // 63 PE features + 1 pad, 32 per lane half
 constexpr int kDirSlots = 32;  // 27 dir-PE features + 5 pad, 16 per lane half
 constexpr int kBlockBytes = 1024;        // one A-fragment block (64 lanes x 16 B)
-#ifndef CN_CHUNK_BLOCKS
-#define CN_CHUNK_BLOCKS 16
-#endif
-constexpr int kChunkBlocks = CN_CHUNK_BLOCKS;   // LDS ring slot = 16 blocks = 16 KiB (one barrier per slot)
+constexpr int kChunkBlocks = 16;   // LDS ring slot = 16 blocks = 16 KiB (one barrier per slot)
 constexpr int kChunkBytes = kBlockBytes * kChunkBlocks;
 
 // Reference parameter tensor indices (state_dict order, oracle/params.py).

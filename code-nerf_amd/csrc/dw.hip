@@ -23,15 +23,6 @@
 #include "chain_args.h"
 #include "dw_args.h"
 
-#ifndef CN_DW_NT
-#define CN_DW_NT 1      // non-temporal policy on the once-read operand stream (A/B: 3.24 -> 3.13 ms per C2 dW)
-#endif
-#ifndef CN_DW_NOROT
-#define CN_DW_NOROT 0   // A/B: every workgroup walks its slabs from the start of its share
-#endif
-#ifndef CN_DW_ILV
-#define CN_DW_ILV 0     // A/B: pieces interleaved across waves (8 KiB contiguous per DMA round)
-#endif
 
 namespace cn {
 
@@ -107,9 +98,6 @@ struct DwBody {
 
   __device__ static void run(const DwProblem& pr, int t0, int t1, int rot, float* part, float* dbpart, char* smem) {
     const int nst = t1 - t0;
-#if CN_DW_NOROT
-    rot = 0;
-#endif
     rot %= nst;
     auto slab = [&](int st) { const int t = st + rot; return t0 + (t >= nst ? t - nst : t); };
     const int lane = threadIdx.x & 63;
@@ -136,11 +124,7 @@ struct DwBody {
       const size_t t = (size_t)slab(st);
 #pragma unroll
       for (int k = 0; k < kG; ++k) {
-#if CN_DW_ILV
-        const int piece = k * 8 + w;             // wave-uniform; one DMA round = 8 consecutive KiB
-#else
         const int piece = w * kG + k;            // wave-uniform
-#endif
         const char* src;
         uint32_t dst = lds_addr(smem + decltype(slotc)::value * kDwSlot + piece * 1024);
         if (piece < kPA) src = pa + t * (kA * TB) + piece * 1024;
@@ -150,11 +134,9 @@ struct DwBody {
           src = pa + t * (kA * TB);              // padding piece: re-read, never consumed
           dst = lds_addr(smem + kDwDummy + (piece - kPieces) * 1024);
         }
-#if CN_DW_NT
+        // non-temporal: a once-read stream (measured 3.24 -> 3.13 ms per C2 dW
+        // against the default policy)
         glds16_opaque_nt(src + lane * 16, dst);
-#else
-        glds16_opaque(src + lane * 16, dst);
-#endif
       }
     };
     static_for<0, kDwDepth>([&](auto i) {

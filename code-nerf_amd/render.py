@@ -45,6 +45,9 @@ class ImageStep:
         self.recompute = False
         self._ws = {}                            # device -> grow-only workspace
         self._side = {}                          # device -> side stream
+        # called whenever a step starts writing .grad (dp.GradExchange's
+        # mark_dirty: a fused zero-grad AdamW step must not mask them)
+        self.grad_listeners = []
 
     # ------------------------------------------------------------ resources
     def _workspace(self, eng, M):
@@ -108,6 +111,10 @@ class ImageStep:
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
         return [p.grad for p in tensors]
+
+    def _writing_grads(self):
+        for f in self.grad_listeners:
+            f()
 
     # ------------------------------------------------------------ backward
     def _bwd_dw(self, eng, blob, ws, zvec, gtab, M):
@@ -183,6 +190,7 @@ class ImageStep:
         params = self.model.param_list()
         grads = self.ensure_grads(params)
         self.ensure_grads([shape_table, texture_table])
+        self._writing_grads()
         R = rays_o.shape[0]
         N = z.shape[-1]
         M = R * N
@@ -255,6 +263,7 @@ class ImageStep:
         params = self.model.param_list()
         grads = self.ensure_grads(params)
         self.ensure_grads([shape_table, texture_table])
+        self._writing_grads()
         R = rays_o.shape[0]
         Nc = z_c.shape[-1]
         Nf = rand_f.shape[-1]

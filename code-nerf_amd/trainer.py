@@ -69,6 +69,7 @@ class Trainer:
         self.step_impl = ImageStep(self.model, chunk=self.B, reg_coef=self.hpams["loss_reg_coef"])
         self.exchange = dp.GradExchange(self.model.param_list(), [self.shape_codes.weight, self.texture_codes.weight],
                                         dist)
+        self.step_impl.grad_listeners.append(self.exchange.mark_dirty)     # every .grad write re-arms zero()
         self.n_fine = int(self.hpams.get("N_importance", 0))
         self.psnr_log = []
 
@@ -116,7 +117,6 @@ class Trainer:
                 else:
                     loss_per_img, rgb, reg = self.step_impl.forward_backward(
                         rays_o, viewdir, z, gt, self.shape_codes.weight, self.texture_codes.weight, oi)
-                self.exchange.mark_dirty()                          # the next zero() must clear them
             self.exchange.exchange_rows([oi], 1)          # data parallel: the touched code rows,
             work = self.exchange.start_model()           # then the async model all-reduce
             self.opts.step(groups=[1, 2], zero_grad=True)  # the kernel leaves the gradients at 0:

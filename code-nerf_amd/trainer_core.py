@@ -19,7 +19,8 @@ from .render import ImageStep
 
 class TrainCore:
     def __init__(self, model, shape_codes, texture_codes, near, far, n_coarse, n_fine=0, chunk=2048,
-                 reg_coef=1e-4, lr=(1e-4, 1e-3), timers=None, dist=None, step_opts=None, zero_grad_in_adamw=True):
+                 reg_coef=1e-4, lr=(1e-4, 1e-3), timers=None, dist=None, step_opts=None, zero_grad_in_adamw=True,
+                 rows_per_step=1):
         self.model = model
         self.shape_codes = shape_codes
         self.texture_codes = texture_codes
@@ -29,6 +30,12 @@ class TrainCore:
         self.dist = dist
         self.step_impl = ImageStep(model, chunk=chunk, reg_coef=reg_coef, timers=timers, **(step_opts or {}))
         self.exchange = GradExchange(model.param_list(), [shape_codes, texture_codes], dist)
+        # any write into .grad (a direct ImageStep call included) re-arms zero()
+        self.step_impl.grad_listeners.append(self.exchange.mark_dirty)
+        # code rows each rank may exchange per step: every rank pads its rows
+        # to this SAME constant, so the all_gather sizes agree without a
+        # count exchange (exchange_rows raises past it)
+        self.rows_per_step = int(rows_per_step)
         self.bucket = self.exchange.bucket
         self.flat_grad = self.bucket.flat
         # the AdamW kernel leaves the gradients it consumed at 0, so the next
@@ -77,7 +84,7 @@ class TrainCore:
         tables take their AdamW step while it is in flight; then the model's
         AdamW step."""
         self.exchange.mark_dirty()     # a backward filled the gradients
-        self.exchange.exchange_rows(rows, len(rows))
+        self.exchange.exchange_rows(rows, self.rows_per_step)
         work = self.exchange.start_model()
         zg = self.zero_grad_in_adamw
         self.opt.step(groups=[1, 2], zero_grad=zg)

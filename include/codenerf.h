@@ -165,7 +165,8 @@ int cn_mlp_dbias(const cn_plan *plan, void *d_act, int act_M, int M, float *d_db
                  void *stream);
 
 /* ---- latent layers + code gradients (+ the code regulariser of
- * src/trainer.py:76-78 when reg_coef != 0; d_reg_out += reg value).
+ * src/trainer.py:76-78 when reg_coef != 0; *d_reg_out = reg value:
+ * written, not accumulated; 0 when reg_coef == 0).
  * d_scratch: num_inject x 256 floats.  d_dshape / d_dtex accumulate. */
 int cn_latent_bwd(const cn_plan *plan, const float *const *d_params, float *const *d_grads,
                   const float *d_shape_code, const float *d_texture_code, const float *d_zvec,

@@ -83,12 +83,13 @@ def positional_encoding(x, n_freq):
 # fp32 accumulator), so they stay fp32 here.  Off by default: the oracle is
 # the fp32 reference; ``bf16_operands()`` switches a block of code over.
 #
-# ``split_w`` restates the error-compensated mode ("bf16x2", precision
-# "bf16s"): every weight is carried as W_hi + W_lo (two bf16, W_hi = rn(W),
-# W_lo = rn(W - W_hi)) and both halves multiply the same bf16 operand into
-# one fp32 accumulator, in the forward and in dX; dW is unchanged.
-# ``split_x`` / ``split_dy`` additionally split the layer inputs / upstream
-# gradients the same way.  ``ops`` sets each operand separately, for the
+# ``split_w`` carries every weight as W_hi + W_lo (two bf16, W_hi = rn(W),
+# W_lo = rn(W - W_hi)) in the forward and in dX; ``split_x`` / ``split_dy``
+# additionally split the layer inputs / upstream gradients the same way.
+# The bf16x3 kernels (precision "bf16x3", OPS_BF16X3 below) split weights and
+# chain operands and issue three MFMAs per block, hi*hi + hi*lo + lo*hi (the
+# dropped lo*lo term is ~2^-16 relative): the sum of the split operands is
+# what _q(.., "s") forms.  ``ops`` sets each operand separately, for the
 # emulation probes (tools/split_emu.py): keys fw_w, fw_x (forward), bw_w,
 # bw_dy (dX), dw_x, dw_dy (dW); values "b" (bf16), "s" (hi + lo), "f" (fp32).
 _OPS_BF16 = dict(fw_w="b", fw_x="b", bw_w="b", bw_dy="b", dw_x="b", dw_dy="b")
@@ -102,11 +103,23 @@ def _rb(t):
     return t.to(torch.bfloat16).to(torch.float32)
 
 
-def _q(t, how):
+def _rh(t):
+    return t.to(torch.float16).to(torch.float32)
+
+
+def _q(t, how, scale=1.0):
     """t as an operand: "b" bf16-rounded, "s" hi + lo bf16 pair summed in
-    fp32 (exact: <= 16 significant bits), "f" unchanged."""
+    fp32 (exact: <= 16 significant bits), "h" fp16-rounded, "hs" hi + lo
+    fp16 pair (IEEE fp16 incl. subnormals: ~22 bits in range), "f"
+    unchanged.  ``scale`` (a power of two) multiplies t before an fp16
+    rounding and divides after (the backward's gradient scale)."""
     if how == "f":
         return t
+    if how in ("h", "hs"):
+        u = t * scale
+        hi = _rh(u)
+        r = hi + _rh(u - hi) if how == "hs" else hi
+        return r / scale
     hi = _rb(t)
     return hi + _rb(t - hi) if how == "s" else hi
 
@@ -122,15 +135,16 @@ class _Bf16Linear(torch.autograd.Function):
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
         o = ctx.o
-        dx = _q(dy, o["bw_dy"]) @ _q(w, o["bw_w"])
-        d2 = _q(dy, o["dw_dy"]).reshape(-1, dy.shape[-1])
+        gs = o.get("grad_scale", 1.0)
+        dx = _q(dy, o["bw_dy"], gs) @ _q(w, o["bw_w"])
+        d2 = _q(dy, o["dw_dy"], gs).reshape(-1, dy.shape[-1])
         x2 = _q(x, o["dw_x"]).reshape(-1, x.shape[-1])
         return dx, d2.t() @ x2, d2.sum(0), None
 
 
 class bf16_operands:
     """with ref_cpu.bf16_operands(): ... -- the bf16 kernels' arithmetic;
-    ``bf16_operands(split_w=True)`` the compensated bf16x2 kernels'."""
+    ``bf16_operands(ops=OPS_BF16X3)`` the bf16x3 kernels'."""
 
     def __init__(self, split_w=False, split_x=False, split_dy=False, ops=None, layer_ops=None):
         o = dict(_OPS_BF16)

@@ -240,3 +240,27 @@ def test_exchange_rows_dedups_and_pads_unequal_counts():
     want[3] = 2 * base[3]        # rank 1's row 3 (its grads are 2x)
     np.testing.assert_array_equal(sg, want)
     np.testing.assert_array_equal(tg, want)
+
+
+def test_zero_after_fused_zero_grad_step_clears_direct_backward_writes():
+    """a fused zero-grad AdamW step sets GradExchange.clean so the
+    next zero() skips its launch; a backward that writes .grad WITHOUT going
+    through TrainCore.step_grads (ImageStep.forward_backward called
+    directly) must re-arm it -- ImageStep notifies its grad_listeners."""
+    from codenerf_amd.dp import GradExchange
+    from codenerf_amd.render import ImageStep
+    params = [torch.zeros(4, 3), torch.zeros(5)]
+    table = torch.zeros(6, 2)
+    ex = GradExchange(params, [table])
+    step = ImageStep(model=None)
+    step.grad_listeners.append(ex.mark_dirty)
+    ex.clean = True                     # as after a zero_grad AdamW step
+    step._writing_grads()               # what _coarse_part / _fine_part do before writing
+    params[0].grad.fill_(1.0)
+    table.grad.fill_(2.0)
+    ex.zero()
+    assert float(params[0].grad.abs().sum()) == 0.0 and float(table.grad.abs().sum()) == 0.0
+    # without a write in between, the clean flag still saves the launch once
+    ex.clean = True
+    ex.zero()
+    assert ex.clean is False

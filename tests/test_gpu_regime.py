@@ -9,8 +9,9 @@ identical initial weights and RNG draws through:
 
   * the HIP trainer in fp32 (the reference precision),
   * the HIP trainer in bf16 (BASELINE C2's operand precision),
-  * the HIP trainer in bf16s (error-compensated: weights carried as
-    bf16 hi + lo pairs, two MFMAs per block into one fp32 accumulator),
+  * the HIP trainer in bf16x3 (error-compensated: weights AND chain
+    operands carried as bf16 hi + lo pairs, three MFMAs per block --
+    hi*hi + hi*lo + lo*hi -- into one fp32 accumulator),
   * the fp32 CPU replay of the reference loop (oracle/ref_cpu.py),
 
 and asserts each one's per-step train PSNR (src/trainer.py:98-101) against the

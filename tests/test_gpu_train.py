@@ -30,16 +30,19 @@ def _hpams(root, N=16, prec="fp32", n_train_views=4, n_test_views=3):
             "check_points": 1000, "N_importance": 0, "precision": prec}
 
 
-def _oracle_training(hp, init, iters_all, B, n_inst=1, iters_crop=0):
+def _oracle_training(hp, init, iters_all, B, n_inst=1, iters_crop=0, device=None):
     """CPU replay of src/trainer.py:34-96 with the oracle's image step: crop
     phase (central 64x64 of a 128^2 view, focal unchanged, src/data.py:76-78) while niter < iters_crop, AdamW re-created
     per epoch, zero_grad inside the per-image loop (only the last of the
-    n_inst images drives the step, src/trainer.py:61-64)."""
+    n_inst images drives the step, src/trainer.py:61-64).  ``device``: run
+    the replay's tensors there (tools/split_emu.py on a GPU box); the random
+    draws stay on the host generator, so they are the same."""
     from codenerf_amd.data import SRN, collate_one
     from oracle import ref_cpu
-    p = {k: v.clone().requires_grad_() for k, v in init["model"].items()}
-    st = init["shape"].clone().requires_grad_()
-    tt = init["texture"].clone().requires_grad_()
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    p = {k: v.to(dev).clone().requires_grad_() for k, v in init["model"].items()}
+    st = init["shape"].to(dev).clone().requires_grad_()
+    tt = init["texture"].to(dev).clone().requires_grad_()
     d = hp["data"]
     psnrs, niter, shapes = [], 0, []
     while niter < iters_all:
@@ -59,8 +62,8 @@ def _oracle_training(hp, init, iters_all, B, n_inst=1, iters_crop=0):
                     t.grad = None
                 ro, vd = ref_cpu.get_rays(int(H), int(W), focal, poses[0, k])
                 z = ref_cpu.stratified_z(hp["near"], hp["far"], hp["N_samples"])
-                losses, _ = ref_cpu.image_step(p, st, tt, int(oi), ro, vd, z, imgs[0, k], chunk=B,
-                                               reg_coef=hp["loss_reg_coef"])
+                losses, _ = ref_cpu.image_step(p, st, tt, int(oi), ro.to(dev), vd.to(dev), z.to(dev),
+                                               imgs[0, k].to(dev), chunk=B, reg_coef=hp["loss_reg_coef"])
             opt.step()
             psnrs.append(-10 * np.log(np.mean(losses)) / np.log(10))
             shapes.append(int(H))

@@ -5,7 +5,7 @@
 #   bash tools/gpu_stalls.sh TAG PRECISION [CODENERF_LIB]
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out; mkdir -p $O; cd /tmp && export TMPDIR=/tmp
-TAG=$1; PREC=$2; export CODENERF_LIB=${3:-}
+TAG=$1; PREC=$2; export CODENERF_LIB=${3:-} CODENERF_MEASURE=1
 rm -rf $O/${TAG}_s1 $O/${TAG}_s2
 KB="$R/tools/kbench.py --only fwd,bwd --reps 3 --precision $PREC"
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_VALU_MFMA_COEXEC_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE --output-format csv -d $O/${TAG}_s1 -- python3 $KB > $O/${TAG}_s1.log 2>&1 || { tail -5 $O/${TAG}_s1.log; exit 1; }

@@ -13,7 +13,7 @@ TAG=$1; TARGETS=$2; FULL=$3
 for p in ${KB_PRECS-bf16 bf16x3}; do
   for v in default $KB_VARIANTS; do
     lib=""; [ "$v" != default ] && lib=$R/code-nerf_amd/libcodenerf_hip_$v.so
-    CODENERF_LIB=$lib timeout -k 10 180 python -u tools/kbench.py --precision $p --only fwd,bwd,dw > $O/kb_${TAG}_${p}_$v.log 2>&1 \
+    CODENERF_MEASURE=1 CODENERF_LIB=$lib timeout -k 10 180 python -u tools/kbench.py --precision $p --only fwd,bwd,dw > $O/kb_${TAG}_${p}_$v.log 2>&1 \
       || { echo "kbench $p $v failed"; tail -20 $O/kb_${TAG}_${p}_$v.log; exit 1; }
     echo "$v $(tail -1 $O/kb_${TAG}_${p}_$v.log)"
   done

@@ -11,6 +11,10 @@ Two regimes:
           across the objects of an epoch; src/trainer.py:48-96).
 
   python tools/split_emu.py one|many [steps] [init seed; < 0: numpy-seeded params]
+
+Env: EMU_ONLY=a,b (variants; fp32 always runs), EMU_THREADS, EMU_DEVICE
+(e.g. cuda: the replay's tensors on a GPU -- torch fp32 matmuls, the same
+host random draws), EMU_GS_LOG2 (the fp16 variants' gradient scale).
 """
 import os
 import sys
@@ -24,8 +28,12 @@ sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
 B, S, F = "b", "s", "f"
+GS = float(2 ** int(os.environ.get("EMU_GS_LOG2", "20")))
 VARIANTS = {
     "fp32": None,
+    # fp32 through the emulation's own matmul path (x @ W^T + b instead of
+    # F.linear): a second fp32 summation order -- the chaos floor
+    "f_path": dict(ops=dict(fw_w=F, fw_x=F, bw_w=F, bw_dy=F, dw_x=F, dw_dy=F)),
     "bf16": dict(),
     "split_w": dict(split_w=True),
     "split_wx": dict(split_w=True, split_x=True),
@@ -41,11 +49,36 @@ VARIANTS = {
     "bw_w": dict(ops=dict(bw_w=S)),
     # the forward's W split only (x bf16), dX fully split
     "fwW_bw3": dict(ops=dict(fw_w=S, bw_w=S, bw_dy=S)),
+    # bf16x3 chains + a split dW operand (round-4 verdict item 1)
+    "s3_dwdy": dict(ops=dict(fw_w=S, fw_x=S, bw_w=S, bw_dy=S, dw_dy=S)),
+    "s3_dwx": dict(ops=dict(fw_w=S, fw_x=S, bw_w=S, bw_dy=S, dw_x=S)),
+    "s3_dwall": dict(ops=dict(fw_w=S, fw_x=S, bw_w=S, bw_dy=S, dw_x=S, dw_dy=S)),
+    # fp16 operands ("h": one fp16, "hs": fp16 hi + lo) with the backward's
+    # gradients scaled by GS (a power of two) before rounding
+    "h_all": dict(ops=dict(fw_w="h", fw_x="h", bw_w="h", bw_dy="h", dw_x="h", dw_dy="h", grad_scale=GS)),
+    "h3_dwb": dict(ops=dict(fw_w="hs", fw_x="hs", bw_w="hs", bw_dy="hs", grad_scale=GS)),
+    "h3_dwh": dict(ops=dict(fw_w="hs", fw_x="hs", bw_w="hs", bw_dy="hs", dw_x="h", dw_dy="h", grad_scale=GS)),
+    "h3_dwhs": dict(ops=dict(fw_w="hs", fw_x="hs", bw_w="hs", bw_dy="hs", dw_x="hs", dw_dy="hs", grad_scale=GS)),
+    "h3_noscale": dict(ops=dict(fw_w="hs", fw_x="hs", bw_w="hs", bw_dy="hs", dw_x="h", dw_dy="h")),
 }
+# bf16x3 chains + the dW X split, except ONE layer whose chain operands stay
+# plain bf16 (which layers can skip the three-MFMA cost?); and the split in
+# one chain direction only
+_X3DWX = dict(fw_w=S, fw_x=S, bw_w=S, bw_dy=S, dw_x=S)
+VARIANTS["dwx_fwd_only"] = dict(ops=dict(fw_w=S, fw_x=S, dw_x=S))
+VARIANTS["dwx_bwd_only"] = dict(ops=dict(bw_w=S, bw_dy=S, dw_x=S))
+VARIANTS["dwx_bwd_dy"] = dict(ops=dict(fw_w=S, fw_x=S, bw_dy=S, dw_x=S))
 # per-layer probes: chain_s3 everywhere except one layer in plain bf16
 _LAYERS = ["encoding_xyz.0", "shape_layer_1.0", "shape_layer_2.0", "shape_layer_3.0", "encoding_shape",
            "encoding_viewdir.0", "texture_layer_1.0", "rgb.0", "rgb.2"]
 for _l in _LAYERS:
+    # bf16x3 chains + ONE layer's dW operand split (which layers need it?)
+    VARIANTS["s3_dwx_" + _l.replace(".0", "").replace(".", "")] = dict(ops=dict(fw_w=S, fw_x=S, bw_w=S, bw_dy=S),
+                                                  layer_ops={_l: dict(dw_x=S)})
+    VARIANTS["s3_dwdy_" + _l.replace(".0", "").replace(".", "")] = dict(ops=dict(fw_w=S, fw_x=S, bw_w=S, bw_dy=S),
+                                                   layer_ops={_l: dict(dw_dy=S)})
+    VARIANTS["dwx_but_" + _l.replace(".0", "").replace(".", "")] = dict(
+        ops=dict(_X3DWX), layer_ops={_l: dict(fw_w=B, fw_x=B, bw_w=B, bw_dy=B)})
     VARIANTS["s3_but_" + _l.split(".")[0]] = dict(ops=dict(fw_w=S, fw_x=S, bw_w=S, bw_dy=S),
                                                   layer_ops={_l: dict(fw_w=B, fw_x=B, bw_w=B, bw_dy=B)})
     VARIANTS["b16_but_" + _l.split(".")[0]] = dict(layer_ops={_l: dict(fw_w=S, fw_x=S, bw_w=S, bw_dy=S)})
@@ -57,7 +90,7 @@ def main():
     from oracle.params import make_params, make_codes
     from test_gpu_train import _oracle_training
     regime = sys.argv[1] if len(sys.argv) > 1 else "one"
-    torch.set_num_threads(os.cpu_count() or 8)
+    torch.set_num_threads(int(os.environ.get("EMU_THREADS", os.cpu_count() or 8)))
     tmp = tempfile.mkdtemp()
     root = os.path.join(tmp, "data")
     if regime == "one":
@@ -82,6 +115,15 @@ def main():
         m = CodeNeRF(**hp["net_hyperparams"])
         init = {"model": {k: v.detach().clone() for k, v in m.state_dict().items()},
                 "shape": torch.randn(n_obj, 256) / np.sqrt(128), "texture": torch.randn(n_obj, 256) / np.sqrt(128)}
+    import threading
+    import time
+
+    def beat():             # progress for a runner that kills silent commands
+        t0 = time.time()
+        while True:
+            time.sleep(60)
+            print(f"[split_emu] {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+    threading.Thread(target=beat, daemon=True).start()
     runs = {}
     only = os.environ.get("EMU_ONLY")
     for name, cfg in VARIANTS.items():
@@ -89,11 +131,12 @@ def main():
             continue
         torch.manual_seed(1000 + max(seed, 0))
         np.random.seed(1000 + max(seed, 0))
+        dev = os.environ.get("EMU_DEVICE")
         if cfg is None:
-            ps, _, _, _ = _oracle_training(hp, init, steps, B)
+            ps, _, _, _ = _oracle_training(hp, init, steps, B, device=dev)
         else:
             with ref_cpu.bf16_operands(**cfg):
-                ps, _, _, _ = _oracle_training(hp, init, steps, B)
+                ps, _, _, _ = _oracle_training(hp, init, steps, B, device=dev)
         runs[name] = np.array(ps)
         print(f"{name:10s}", np.round(runs[name], 3).tolist(), flush=True)
     ref = runs["fp32"]
@@ -101,6 +144,14 @@ def main():
         d = np.abs(v - ref)
         print(f"{k:10s} max |d| vs fp32 {d.max():.4f} dB; first step > 0.05: "
               f"{int(np.argmax(d > 0.05)) if (d > 0.05).any() else None}")
+    if regime != "one":
+        # epoch means (test_gpu_regime.py's long-horizon measure)
+        em = {k: v[: len(v) // n_obj * n_obj].reshape(-1, n_obj).mean(1) for k, v in runs.items()}
+        for k, v in em.items():
+            g = np.abs(v - em["fp32"])
+            first = int(np.argmax(g > 0.05)) if (g > 0.05).any() else None
+            print(f"{k:10s} epoch-mean |d| vs fp32 {np.round(g, 3).tolist()} first epoch > 0.05: {first}",
+                  flush=True)
 
 
 if __name__ == "__main__":
