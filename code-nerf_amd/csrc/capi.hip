@@ -139,6 +139,10 @@ long long cn_act_plane(const cn_plan* p, int M, int kind, int index, int* width)
     w = 32, off = (long long)L.dir;
   } else if (kind == CN_PLANE_MASKS) {
     w = (int)(L.mask_bytes_per_slab / 32), off = (long long)L.masks;
+  } else if (kind == CN_PLANE_YLO && index >= 0 && index < kMaxPlanes && L.Ylo[index]) {
+    w = (int)L.Yw[index], off = (long long)L.Ylo[index];
+  } else if (kind == CN_PLANE_PELO && L.pelo) {
+    w = 64, off = (long long)L.pelo;
   }
   if (width) *width = w;
   return off;
@@ -222,6 +226,8 @@ static int mlp_fwd_impl(int codes, const cn_plan* p, const void* d_pack, const f
     a.d8 = b + L.d8 + r0 * 32 * es;
     a.spre = (float*)(b + L.spre) + r0;
     a.masks = (uint32_t*)(b + L.masks + (r0 / 32) * L.mask_bytes_per_slab);
+    a.pelo = L.pelo ? b + L.pelo + r0 * 64 * es : nullptr;
+    for (int i = 0; i < kMaxPlanes; ++i) a.Ylo[i] = L.Ylo[i] ? b + L.Ylo[i] + r0 * L.Yw[i] * es : nullptr;
   }
   const int grid = (Mp + p->cs.waves_fwd * 32 - 1) / (p->cs.waves_fwd * 32);
   hipLaunchKernelGGL(d_act ? (codes ? p->cs.fwd_codes : p->cs.fwd_train) : p->cs.fwd_infer, dim3(grid),

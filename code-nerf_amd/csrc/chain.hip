@@ -165,6 +165,10 @@ struct Chain {
   static constexpr bool kX3 = (P == CN_P_BF16X3);    // hi + lo operands, three MFMAs per block
   static constexpr bool TRAIN = MODE != CN_MODE_INFER;    // masks + sigma pre-activation
   static constexpr bool PLANES = MODE == CN_MODE_TRAIN;   // every operand plane of dW
+  // bf16x3 training forward: also the lo parts of dW's X operands (PE and
+  // every stored Y plane, from the binl registers the epilogues already
+  // hold), so the weight gradients multiply hi + lo (dw.hip DwBody<..., LO>)
+  static constexpr bool kXlo = kX3 && PLANES && !BWD;
   static constexpr int NL = S::NL;
   static constexpr int kChunks = S::kChunks;
   // waves that issue the weight stream's LDS-DMA (all of them when WAVES
@@ -290,7 +294,7 @@ struct Chain {
       if (!diag(i) && S::last_block(i) == g) s += stores_of_layer(i);
       if (diag(i) && final_block(i) == g) s += final_stores(i);
     }
-    if (deferred_at(g) >= 0) s += 1;
+    if (deferred_at(g) >= 0) s += kXlo ? 2 : 1;
     return s;
   }
   static constexpr int stores_between(int b0, int b1) {
@@ -313,17 +317,37 @@ struct Chain {
       if (wp(c) == g) return c;
     return -1;
   }
+  // Staggered weight stream (8-wave workgroups, two waves per SIMD): waves
+  // w and w + 4 share a SIMD (a workgroup's waves are placed on the SIMDs
+  // cyclically), so waves 4..7 issue their LDS-DMA pieces of chunk c + D
+  // kLateOff blocks after chunk c's wait point instead of right after its
+  // barrier -- the two waves of a SIMD then never stall on DMA issue at the
+  // same time and one keeps the matrix pipe fed.  Still safe: the refilled
+  // slot (chunk c - 2's) stays free until the next barrier at least.
+  // (the dX chain only: the 8-wave forward sits at the 256-register limit,
+  // and the issue branches pushed it into scratch)
+  static constexpr bool kStagger = WAVES == 8 && kBf16 && BWD;
+  static constexpr int kLateOff = kChunkBlocks / 2;
+  static constexpr int lp(int c) { return wp(c) + kLateOff; }   // late issue point of chunk c + D
+  static constexpr int late_chunk_at(int g) {
+    for (int c = 0; c < kChunks; ++c)
+      if (c + D < kChunks && lp(c) == g) return c;
+    return -1;
+  }
   // Younger VMEM ops that may still be in flight at chunk c's wait point:
-  // the LDS-DMAs issued after chunk c's and the stores issued since it.
-  static constexpr int vm_wait(int c) {
+  // the LDS-DMAs issued after chunk c's and the stores issued since it (an
+  // issue point's DMAs go out before that block's stores).  late: the
+  // counts of a wave that issues at lp() instead of wp().
+  static constexpr int vm_wait(int c, bool late = false) {
+    auto at = [&](int w) { return late ? lp(w) : wp(w); };
     int n = 0;
     if (c < D) {
       for (int i = c + 1; i < D; ++i) n += issued(i);        // the initial issue, younger than c
-      for (int w = 0; w < c; ++w) n += issued(w + D);        // wait points 0 .. c-1
+      for (int w = 0; w + D < kChunks && at(w) < wp(c); ++w) n += issued(w + D);
       n += stores_between(0, wp(c));
     } else {
-      for (int w = c - D + 1; w < c; ++w) n += issued(w + D);
-      n += stores_between(wp(c - D), wp(c));
+      for (int w = c - D + 1; w + D < kChunks && at(w) < wp(c); ++w) n += issued(w + D);
+      n += stores_between(at(c - D), wp(c));
     }
     return n;
   }
@@ -396,13 +420,24 @@ struct Chain {
       constexpr int g = gc;
       constexpr int wc = wait_chunk_at(g);
       if constexpr (wc >= 0) {
-        wait_vmcnt<vm_wait(wc)>();
+        // a late wave has fewer younger VMEM ops in flight than an early
+        // one (its DMA went out after some of the stores): its count serves
+        // both (an early wave then also waits for stores >= 2 chunks old)
+        wait_vmcnt<vm_wait(wc, kStagger)>();
         block_barrier_noread();
-        if constexpr (wc + D < kChunks) issue<wc + D>(a, smem, w, lane);
+        if constexpr (wc + D < kChunks) {
+          if (!kStagger || w < 4) issue<wc + D>(a, smem, w, lane);
+        }
         if constexpr (wc == 0 && kBf16)
           static_for<0, kPF>([&](auto bb) {
             if constexpr (bb < S::kBlocks) aread(bb);
           });
+      }
+      if constexpr (kStagger) {
+        constexpr int lc = late_chunk_at(g);
+        if constexpr (lc >= 0) {
+          if (w >= 4) issue<lc + D>(a, smem, w, lane);
+        }
       }
       constexpr int li = S::layer_of(g);
       constexpr int lb = g - S::first_block(li);
@@ -463,6 +498,11 @@ struct Chain {
         const u32x4 b = bin[j];                    // tile j / 2, pair j % 2
         plane_store_pair(slab_rsrc<E>(BWD ? a.dA[plane] : a.Y[plane], F, wglob), voff[4 + (j & 1)], j >> 1,
                          u32x2{b[0], b[1]}, u32x2{b[2], b[3]});
+        if constexpr (kXlo) {
+          const u32x4 bl = binl[j];
+          plane_store_pair(slab_rsrc<E>(a.Ylo[plane], F, wglob), voff[4 + (j & 1)], j >> 1, u32x2{bl[0], bl[1]},
+                           u32x2{bl[2], bl[3]});
+        }
       }
     };
     // (two nested loops: one static_for over ~300 blocks would exceed the
@@ -597,6 +637,16 @@ struct Chain {
 #pragma unroll
       for (int k = 0; k < 4; ++k)
         plane_store<E>(rd, voff, 0, k, dp[4 * k], dp[4 * k + 1], dp[4 * k + 2], dp[4 * k + 3]);
+      if constexpr (kXlo) {
+        // the PE operand's lo parts (the dir-PE tile of encoding_viewdir's
+        // dW stays hi only: its staged slab would not fit the LDS ring)
+        auto lo = [](float x) { return x - (float)(__bf16)x; };
+        const auto rpl = slab_rsrc<E>(a.pelo, 64, wglob);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          plane_store<E>(rpl, voff, k >> 2, k & 3, lo(pe[4 * k]), lo(pe[4 * k + 1]), lo(pe[4 * k + 2]),
+                         lo(pe[4 * k + 3]));
+      }
     }
   }
 
@@ -667,6 +717,9 @@ struct Chain {
                                       int h, int wglob, const uint32_t* voff, float& sig_part, MaskAcc& mk) {
     constexpr Layer l = S::L(LI);
     constexpr int t = TT;
+    // tile t of this layer starts tile t of the next one (bias, below): every
+    // next-layer tile has a tile here only while the next layer is no wider
+    static_assert(LI + 1 >= NL || S::L(LI + 1).T <= l.T, "next layer wider than this one: its extra tiles get no bias");
     if constexpr (t == 0)
 #pragma unroll
       for (int k = 0; k < 4; ++k) mk.lo[k] = mk.hi[k] = 0u;

@@ -48,6 +48,8 @@ struct ChainArgs {
   void* dir;               // [Mp][32]
   void* Y[kMaxPlanes];     // forward layer outputs
   void* dA[kMaxPlanes];    // pre-activation gradients
+  void* pelo;              // bf16x3: lo parts of pe       (or null)
+  void* Ylo[kMaxPlanes];   // bf16x3: lo parts of every Y  (or null)
   void* d8;                // [Mp][32] drgb (padded)
   float* spre;             // [Mp] sigma-head pre-activation
   uint32_t* masks;         // [Mp/32][kMasks][64][4] pre-activation sign bits

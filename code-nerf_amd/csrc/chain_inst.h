@@ -17,6 +17,10 @@ struct LatentBwdArgs;
 
 struct ActLayout {
   size_t pe = 0, dir = 0, Y[kMaxPlanes] = {}, dA[kMaxPlanes] = {}, d8 = 0, spre = 0, masks = 0, bytes = 0;
+  // bf16x3 only: the lo parts (rn(x - rn(x))) of the dW pass's X operands --
+  // the PE plane and every stored Y plane -- so dW multiplies hi + lo
+  // (0 = absent: the plane is not allocated)
+  size_t pelo = 0, Ylo[kMaxPlanes] = {};
   size_t Yw[kMaxPlanes] = {}, dAw[kMaxPlanes] = {};   // plane widths (elements per sample)
   size_t mask_bytes_per_slab = 0;                     // per 32-sample slab
 };

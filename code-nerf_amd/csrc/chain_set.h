@@ -97,6 +97,12 @@ ActLayout act_layout(size_t Mp) {
   L.spre = take(Mp * 4);
   L.mask_bytes_per_slab = (size_t)N::kMasks * 64 * 16;
   L.masks = take(Mp / 32 * L.mask_bytes_per_slab);
+  if constexpr (P == CN_P_BF16X3) {
+    // the X operands' lo parts, after everything else (the planes above keep
+    // their offsets in every precision)
+    L.pelo = take(Mp * 64 * es);
+    for (int p = 0; p < N::kPlanes; ++p) L.Ylo[p] = L.Yw[p] ? take(Mp * L.Yw[p] * es) : 0;
+  }
   L.bytes = off;
   return L;
 }
@@ -157,6 +163,12 @@ int dw_setup(char* act, int act_M, int row0, int M, int nwg_req, const float* zv
     else { p.x0_width = N::plane_width(xin); p.X0 = act + A.Y[xin] + r0 * p.x0_width; }
     p.x0_tiles = p.x0_width / 32;
     if (vd) { p.X1 = act + A.dir + r0 * 32; p.x1_width = 32; p.x1_tiles = 1; }
+    // bf16x3: X0's lo parts (the training forward stored them, act_layout)
+    const size_t lo_off = L == 0 ? A.pelo : A.Ylo[xin];
+    if (lo_off) {
+      p.X0lo = act + lo_off + r0 * p.x0_width;
+      p.lo = 1;
+    }
     p.sigma_head = vd ? 1 : 0;
     p.kind = L == 0 ? DW_PE : vd ? DW_VIEWDIR : last ? DW_RGB2 : (L == N::kFwdLayers - 2 ? DW_RGB0 : DW_FULL);
     {
@@ -165,7 +177,7 @@ int dw_setup(char* act, int act_M, int row0, int M, int nwg_req, const float* zv
       const int* e = shape[p.kind];
       if (p.a_tiles != e[0] || p.x0_tiles != e[1] || p.x1_tiles != e[2] || p.out_tiles != e[3]) return -1;
     }
-    dw->pbytes[k] = (p.a_tiles + p.x0_tiles + p.x1_tiles) * 1024 * ES;
+    dw->pbytes[k] = (p.a_tiles + p.x0_tiles * (1 + p.lo) + p.x1_tiles) * 1024 * ES;
     dw->wprefix[k] = wsum;
     const long long tot = (long long)dw->pbytes[k] * dw->total_tiles;
     wsum += tot;

@@ -25,6 +25,10 @@ typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
 enum { CN_P_FP32 = 0, CN_P_BF16 = 1, CN_P_BF16X3 = 2 };
 
 // Compile-time for loop: f(std::integral_constant<int, I>) for I in [0, N).
+// Recursive on purpose: every level is a forceinline function, so the chain
+// kernels' register arrays captured by the loop bodies stay in registers (a
+// fold-expression version left the bodies un-inlined and the arrays in
+// scratch).  The deep instantiation needs a large compiler stack (Makefile).
 template <int Begin, int End, class F>
 CN_DEV void static_for(F&& f) {
   if constexpr (Begin < End) {

@@ -172,9 +172,12 @@ inline constexpr int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 *
 //
 // fp32 (16 B = 4 features): per 8-feature group g, 64 "positions" of 4
 // consecutive features; sample s, feature half hh = (f >> 2) & 1 sits at
-//     pos = ((s + 8 g + 4 hh) & 31) + 32 hh,
+//     pos = ((s + g + 4 hh) & 31) + 32 hh,
 // so one epilogue store instruction (lane = s + 32 h writes features
-// 32t + 8g + 4h .. +3) fills one contiguous 64 x 16 B block.
+// 32t + 8g + 4h .. +3) fills one contiguous 64 x 16 B block, and the fp32 dW
+// pass's ds_read_b32 of one sample's 32 tile features (lane c: g = c >> 3,
+// hh = (c >> 2) & 1) hits bank 4 ((s + g + 4 hh) mod 8) + (c & 3): all 32
+// banks (a rotation by 8 g put the four groups on the same 8 banks: 4-way).
 //
 // bf16 (16 B = 8 features): per 16-feature pair block gp, 64 positions of 8
 // consecutive features 16 gp + 8 gg .. +7; sample s sits at
@@ -184,7 +187,7 @@ inline constexpr int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 *
 // whole 1 KiB pair block.  The rotation by 8 gp + 4 gg makes the dW kernel's
 // transposed LDS reads (ds_read_b64_tr_b16: 4 samples x 4 features per lane,
 // a 32-lane half spanning 4 samples x 32 features) hit 64 distinct banks.
-inline constexpr int tile_pos(int s, int g, int hh) { return ((s + 8 * g + 4 * hh) & 31) + 32 * hh; }
+inline constexpr int tile_pos(int s, int g, int hh) { return ((s + g + 4 * hh) & 31) + 32 * hh; }
 inline constexpr int bf16_pos(int s, int gp, int gg) { return 32 * gg + ((s + 8 * gp + 4 * gg) & 31); }
 // byte offset, inside a 32-sample slab, of features f .. f+3 (f % 4 == 0) of sample s
 inline constexpr int slab_off(int s, int f, int es) {

@@ -56,19 +56,30 @@ template <> struct DwShape<DW_RGB2>    { static constexpr int kA = 1, kX0 = 4, k
 // 256x256 bodies measured 0.2 ms slower per C2 step.
 constexpr int kDwSmem = 160 * 1024;
 
-template <int P, int KIND>
+// LO (bf16x3 planes): the slab also stages X0's lo parts (after X1), and every
+// X0 fragment's MFMA is followed by one with the lo fragment, so dW sums
+// A (x) (X0_hi + X0_lo) -- the X operand at ~16 significant bits, as the
+// bf16x3 chains used it.  The dir-PE tile (X1) stays hi only.
+template <int P, int KIND, bool LO = false>
 struct DwBody {
   using Sh = DwShape<KIND>;
   static constexpr bool kBf16 = P == CN_P_BF16;
+  static_assert(kBf16 || !LO, "lo planes exist for bf16 planes only");
   static constexpr int ES = kBf16 ? 2 : 4;
   static constexpr int TB = 1024 * ES;                      // one 32-sample x 32-feature tile
   static constexpr int kA = Sh::kA, kX0 = Sh::kX0, kX1 = Sh::kX1, NI = Sh::NI, NJ = Sh::NJ;
+  static constexpr int kXl = LO ? kX0 : 0;                  // lo tiles of X0
   static constexpr int kPA = kA * TB / 1024, kPX0 = kX0 * TB / 1024;   // 1 KiB pieces of A / X0
-  static constexpr int kPieces = (kA + kX0 + kX1) * TB / 1024;       // 1 KiB pieces per slab
+  static constexpr int kPX1 = kX1 * TB / 1024;
+  static constexpr int kPieces = (kA + kX0 + kX1 + kXl) * TB / 1024;     // 1 KiB pieces per slab
   static constexpr int kG = (kPieces + 7) / 8;              // pieces per wave per slab
   static constexpr bool kVD = KIND == DW_VIEWDIR;
-  static constexpr int kDwSlot = kBf16 ? (KIND == DW_FULL ? 32 * 1024 : 36 * 1024) : 72 * 1024;
-  static constexpr int kDwRing = kBf16 ? 4 : 2;
+  // hi-only bf16: 32 / 36 KiB slots, 4-slot ring (measured best); LO: the
+  // slab itself, as many slots (<= 4) as fit beside the padding pieces
+  static constexpr int kLoRing = (kDwSmem - (8 * kG - kPieces) * 1024) / (kPieces * 1024);
+  static constexpr int kDwSlot = LO ? kPieces * 1024 : kBf16 ? (KIND == DW_FULL ? 32 * 1024 : 36 * 1024) : 72 * 1024;
+  static constexpr int kDwRing = LO ? (kLoRing < 4 ? kLoRing : 4) : kBf16 ? 4 : 2;
+  static_assert(!LO || kDwRing >= 3, "a LO slab must leave a 3-slot ring");
   static constexpr int kDwDepth = kDwRing - 1;        // slabs in flight while one is consumed
   static constexpr int kDwDummy = kDwRing * kDwSlot;  // landing area of padding pieces
   static_assert(kPieces * 1024 <= kDwSlot, "dw stage");
@@ -120,6 +131,7 @@ struct DwBody {
     const char* pa = (const char*)pr.A;
     const char* px0 = (const char*)pr.X0;
     const char* px1 = kX1 ? (const char*)pr.X1 : px0;
+    const char* px0l = LO ? (const char*)pr.X0lo : px0;
     auto issue = [&](int st, auto slotc) {
       const size_t t = (size_t)slab(st);
 #pragma unroll
@@ -129,7 +141,8 @@ struct DwBody {
         uint32_t dst = lds_addr(smem + decltype(slotc)::value * kDwSlot + piece * 1024);
         if (piece < kPA) src = pa + t * (kA * TB) + piece * 1024;
         else if (piece < kPA + kPX0) src = px0 + t * (kX0 * TB) + (piece - kPA) * 1024;
-        else if (piece < kPieces) src = px1 + t * (kX1 * TB) + (piece - kPA - kPX0) * 1024;
+        else if (piece < kPA + kPX0 + kPX1) src = px1 + t * (kX1 * TB) + (piece - kPA - kPX0) * 1024;
+        else if (piece < kPieces) src = px0l + t * (kX0 * TB) + (piece - kPA - kPX0 - kPX1) * 1024;
         else {
           src = pa + t * (kA * TB);              // padding piece: re-read, never consumed
           dst = lds_addr(smem + kDwDummy + (piece - kPieces) * 1024);
@@ -167,6 +180,7 @@ struct DwBody {
       if (st + kDwDepth < nst) issue(st + kDwDepth, std::integral_constant<int, (SL + kDwDepth) % kDwRing>{});
       const char* A = smem + SL * kDwSlot;
       const char* X = A + kA * TB;
+      const char* Xl = X + (kX0 + kX1) * TB;     // LO: X0's lo tiles
       if (!live) return;
       if constexpr (!kBf16) {
         // exact fp32: K = 2 samples per MFMA; lane l reads feature l & 31 of
@@ -228,6 +242,15 @@ struct DwBody {
           for (int i = 0; i < NI; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fx, acc[i][j], 0, 0, 0);
           if constexpr (kVD) {
             if (j == (w >> 1)) acc_e2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fs, fx, acc_e2, 0, 0, 0);
+          }
+          if constexpr (LO) {
+            const bf16x8 fxl = frag(Xl, col_tile(w, j), s);
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fxl, acc[i][j], 0, 0, 0);
+            if constexpr (kVD) {
+              if (j == (w >> 1)) acc_e2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fs, fxl, acc_e2, 0, 0, 0);
+            }
           }
         }
         if constexpr (kVD) {
@@ -295,12 +318,23 @@ __global__ __launch_bounds__(512, 2) void dw_kernel(DwArgs a) {
     const DwProblem& pr = a.p[p];
     float* part = a.part + slot * kPartRows * kPartCols;
     float* dbpart = a.dbpart + slot * kPartRows;
+    // bf16x3 planes: the X0 lo parts ride along (pr.lo, DwBody<..., true>)
+    auto body = [&](auto kind) {
+      constexpr int K = decltype(kind)::value;
+      if constexpr (P == CN_P_BF16) {
+        if (pr.lo) {
+          DwBody<P, K, true>::run(pr, t0, t1, g * 613, part, dbpart, smem);
+          return;
+        }
+      }
+      DwBody<P, K>::run(pr, t0, t1, g * 613, part, dbpart, smem);
+    };
     switch (pr.kind) {
-      case DW_FULL: DwBody<P, DW_FULL>::run(pr, t0, t1, g * 613, part, dbpart, smem); break;
-      case DW_PE: DwBody<P, DW_PE>::run(pr, t0, t1, g * 613, part, dbpart, smem); break;
-      case DW_VIEWDIR: DwBody<P, DW_VIEWDIR>::run(pr, t0, t1, g * 613, part, dbpart, smem); break;
-      case DW_RGB0: DwBody<P, DW_RGB0>::run(pr, t0, t1, g * 613, part, dbpart, smem); break;
-      default: DwBody<P, DW_RGB2>::run(pr, t0, t1, g * 613, part, dbpart, smem); break;
+      case DW_FULL: body(std::integral_constant<int, DW_FULL>{}); break;
+      case DW_PE: body(std::integral_constant<int, DW_PE>{}); break;
+      case DW_VIEWDIR: body(std::integral_constant<int, DW_VIEWDIR>{}); break;
+      case DW_RGB0: body(std::integral_constant<int, DW_RGB0>{}); break;
+      default: body(std::integral_constant<int, DW_RGB2>{}); break;
     }
     ++seg;
   }

@@ -18,6 +18,8 @@ struct DwProblem {
   int x0_width, x0_tiles;
   const void* X1;       // second input plane appended after X0 (dir PE), or null
   int x1_width, x1_tiles;
+  const void* X0lo;     // bf16x3: lo parts of X0 (same layout), staged after X1; null: X0 only
+  int lo;               // 1: X0lo given (dW multiplies A by X0 + X0lo)
   int sigma_head;       // viewdir: also sum ds (A column 256 + 257) x X columns 0..255
   int rows_pad, cols_pad;   // extent of the partial actually written (<= 288)
   int kind;             // DwKind: operand shape, selects the compile-time bf16 body

@@ -77,6 +77,10 @@ size_t cn_dw_ws_bytes(const cn_plan *plan, int M);  /* weight-grad partials */
 #define CN_PLANE_PE 2
 #define CN_PLANE_DIR 3
 #define CN_PLANE_MASKS 4
+/* bf16x3 plans only (-1 otherwise): the lo parts rn(x - rn(x)) of the dW
+ * pass's X operands, stored by the training forward beside the hi planes */
+#define CN_PLANE_YLO 5   /* index: forward layer whose output it is */
+#define CN_PLANE_PELO 6
 long long cn_act_plane(const cn_plan *plan, int M, int kind, int index, int *width);
 
 /* ---- weights: pack the parameters into the chain kernels' fragment order

@@ -93,9 +93,11 @@ def positional_encoding(x, n_freq):
 # emulation probes (tools/split_emu.py): keys fw_w, fw_x (forward), bw_w,
 # bw_dy (dX), dw_x, dw_dy (dW); values "b" (bf16), "s" (hi + lo), "f" (fp32).
 _OPS_BF16 = dict(fw_w="b", fw_x="b", bw_w="b", bw_dy="b", dw_x="b", dw_dy="b")
-# the bf16x3 kernels (chain.hip): weights and layer inputs split in the
-# forward, weights and upstream gradients split in dX, the dW operands bf16
-OPS_BF16X3 = dict(fw_w="s", fw_x="s", bw_w="s", bw_dy="s", dw_x="b", dw_dy="b")
+# the bf16x3 kernels (chain.hip, dw.hip): weights and layer inputs split in
+# the forward, weights and upstream gradients split in dX, the dW pass's X
+# operands split (the training forward stores their lo parts; encoding_viewdir's
+# dir-PE columns stay hi only), its upstream gradients bf16
+OPS_BF16X3 = dict(fw_w="s", fw_x="s", bw_w="s", bw_dy="s", dw_x="s", dw_dy="b")
 _BF16 = {"on": False, "ops": dict(_OPS_BF16)}
 
 

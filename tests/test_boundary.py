@@ -101,3 +101,19 @@ def test_sample_guard_rejects_oversized_calls(fn):
     rc = lib.cn_mlp_bwd_rows(h, d, d, 256, d, d, d, big, 0, None)
     assert rc == -1 and b"CN_MAX_SAMPLES" in lib.cn_last_error()
     lib.cn_plan_destroy(h)
+
+
+def test_hot_kernels_do_not_spill():
+    """Every chain / dW kernel of the shipped library keeps its operands in
+    registers: a scratch-spilling build (e.g. a compiler change that leaves a
+    loop body un-inlined) runs several times slower, so it must not ship
+    (tools/kernel_resources.py reads the code object's metadata)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import kernel_resources as kr
+    if not os.path.exists(kr.LIB):
+        pytest.skip("library not built")
+    ks = kr.kernels()
+    hot = [k for k in ks if "chain_kernel" in k[0] or "dw_kernel" in k[0]]
+    assert len(hot) >= 30, len(hot)
+    assert not [k for k in hot if k[3] > 0], [k for k in hot if k[3] > 0]

@@ -71,7 +71,7 @@ def decode(act, off, F, Mp, dtype):
         elem = slab + gp * 512 + pos * 8 + (f & 7)
     else:           # 8-feature groups of 64 x 4 elements
         g, hh = (f >> 3) & 3, (f >> 2) & 1
-        pos = ((s + 8 * g + 4 * hh) & 31) + 32 * hh
+        pos = ((s + g + 4 * hh) & 31) + 32 * hh
         elem = slab + g * 256 + pos * 4 + (f & 3)
     flat = act[off:off + Mp * F * es].view(dtype)
     return flat[elem].double()
@@ -159,6 +159,21 @@ def test_weight_gradients_match_float64_reduction(precision, R):
         assert eng.L.cn_act_plane(eng._plan, M, kind, SB + 1, None) == -1
     d8 = decode(act, off["d8"], 32, Mp, dtype)
     pe = decode(act, off["pe"], 64, Mp, dtype)
+    if precision == "bf16x3":
+        # dW multiplies the X operands' hi + lo parts (CN_PLANE_YLO / _PELO;
+        # the dir-PE tile stays hi only)
+        import ctypes
+        w = ctypes.c_int()
+        for p in range(N_PLANES):
+            if Y[p] is not None:
+                o = eng.L.cn_act_plane(eng._plan, M, 5, p, ctypes.byref(w))
+                assert o > 0 and w.value == plane_width(p)
+                Y[p] = Y[p] + decode(act, o, w.value, Mp, dtype)
+        o = eng.L.cn_act_plane(eng._plan, M, 6, 0, ctypes.byref(w))
+        assert o > 0 and w.value == 64
+        pe = pe + decode(act, o, 64, Mp, dtype)
+    else:
+        assert eng.L.cn_act_plane(eng._plan, M, 6, 0, None) == -1
     dr = decode(act, off["dir"], 32, Mp, dtype)
     for a in [a for a in dA if a is not None] + [d8]:
         assert torch.count_nonzero(a[M:]) == 0, "padded samples must carry no gradient"

@@ -157,3 +157,81 @@ def test_bf16_planes_match_emulation(M):
     da0 = _bf((da1 @ _bf(P["shape_layer_1.0.weight"])) * (pre0 > 0))
     off0, F0 = plane(1, 0)
     _check("dA0", _decode(act, off0, F0, M), da0)
+
+
+@pytest.mark.parametrize("M", [4096 + 37])
+def test_bf16x3_lo_planes_carry_the_residual(M):
+    """bf16x3 training forward: every X operand of dW is stored as a hi plane
+    and a lo plane (rn(x - rn(x)), CN_PLANE_YLO / CN_PLANE_PELO) so the
+    weight gradients multiply ~16 significant bits.  hi + lo of the PE plane
+    and of Y planes 0, 2, 5, 7 against an fp32 forward (the bf16x3 chains
+    track fp32 to ~2^-16 per layer); a lo plane corrupted by the store hazard
+    or mis-addressed would be off by orders of magnitude."""
+    from codenerf_amd.model import CodeNeRF
+    dev = torch.device("cuda", 0)
+    params = make_params(82)
+    m = CodeNeRF(3, 1, precision="bf16x3")
+    m.load_state_dict({k: torch.tensor(v) for k, v in params.items()})
+    m = m.to(dev)
+    eng = m.engine()
+    P = {k: torch.tensor(v, dtype=torch.float64) for k, v in params.items()}
+    g = torch.Generator().manual_seed(M)
+    xyz = torch.rand(M, 3, generator=g) * 2 - 1
+    vd = torch.nn.functional.normalize(torch.randn(M, 3, generator=g), dim=-1)
+    s0, t0 = (torch.tensor(c[0]) for c in make_codes(82, 1))
+    plist = m.param_list()
+    eng.ensure_packed(plist)
+    blob, _ = eng.latent_fwd(plist, s0.to(dev), t0.to(dev))
+    act = eng.new_act(M)
+    act.zero_()
+    eng.mlp_fwd(blob, M, xyz=xyz.to(dev), viewdir=vd.to(dev), act=act)
+    torch.cuda.synchronize()
+
+    def plane(kind, idx):
+        w = ctypes.c_int()
+        off = eng.L.cn_act_plane(eng._plan, M, kind, idx, ctypes.byref(w))
+        assert off >= 0, (kind, idx)
+        return off, w.value
+
+    def both(kind_hi, kind_lo, idx):
+        off, F = plane(kind_hi, idx)
+        offl, Fl = plane(kind_lo, idx)
+        assert Fl == F
+        hi, lo = _decode(act, off, F, M), _decode(act, offl, F, M)
+        # the lo part is below half a bf16 ulp of the hi part
+        assert bool((lo.abs() <= hi.abs() * 2.0 ** -8 + 1e-30).all())
+        return hi.double() + lo.double()
+
+    def check(name, got, want):
+        scale = want.abs().max().item()
+        d = (got - want).abs()
+        close = (d <= 2e-4 * want.abs() + 1e-5 * scale).double().mean().item()
+        assert close >= 0.99 and d.max().item() <= 1e-3 * scale, (name, close, d.max().item(), scale)
+
+    x64, v64 = xyz.double(), vd.double()
+    pe = _pe(x64, 10)
+    got = both(2, 6, 0)
+    cols = [(c, _pe_slot_feature((c >> 2) & 1, 4 * (c >> 3) + (c & 3))) for c in range(64)]
+    keep = [(c, f) for c, f in cols if f >= 0]
+    check("pe hi+lo", got[:, [c for c, _ in keep]], pe[:, [f for _, f in keep]])
+    d = (got[:, [c for c, _ in keep]] - pe[:, [f for _, f in keep]]).abs()
+    assert d.max().item() <= 2.0 ** -15, d.max().item()      # 16+ significant bits of a |x| <= 2 feature
+
+    def lin(name, x):
+        return x @ P[name + ".weight"].t() + P[name + ".bias"]
+
+    def zinj(kind, j, code):
+        return torch.relu(code.double()[None] @ P[f"{kind}_latent_layer_{j}.0.weight"].t()
+                          + P[f"{kind}_latent_layer_{j}.0.bias"])
+
+    ys = {0: torch.relu(lin("encoding_xyz.0", pe))}
+    for j in range(1, 4):
+        ys[j] = torch.relu(lin(f"shape_layer_{j}.0", ys[j - 1] + zinj("shape", j, s0)))
+    ys[4] = lin("encoding_shape", ys[3])
+    ys[5] = torch.relu(lin("encoding_viewdir.0", torch.cat([ys[4], _pe(v64, 4)], -1)))
+    ys[6] = torch.relu(lin("texture_layer_1.0", ys[5] + zinj("texture", 1, t0)))
+    ys[7] = torch.relu(lin("rgb.0", ys[6]))
+    for i in (0, 2, 5, 7):
+        check(f"Y{i} hi+lo", both(0, 5, i), ys[i])
+    w = ctypes.c_int()
+    assert eng.L.cn_act_plane(eng._plan, M, 5, 4, ctypes.byref(w)) == -1      # encoding_shape: folded

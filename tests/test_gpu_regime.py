@@ -39,7 +39,6 @@ def hp_many(root, prec):
 
 REPLAY_STEPS = 2 * N_OBJ    # CPU replay horizon (two epochs; ~3 s per 262K-sample step on 16 threads)
 LONG_EPOCHS = 40            # HIP-only horizon: every precision against HIP fp32
-X3_EPOCHS = 25              # bf16x3 within 0.05 dB of fp32 (measured round 3: <= 0.008 dB over 28 epochs)
 
 
 def _data(tmp_path):
@@ -106,12 +105,14 @@ def test_many_objects_long_horizon_vs_fp32(tmp_path):
     epoch-mean train PSNR.  Training is chaotic over hundreds of steps (an
     optimiser re-created per epoch, sign-like first steps): the noise floor is
     HIP fp32 against ITSELF with a different fp32 summation order (the dW
-    pass run in one range instead of two pipelined ones).  Asserted: bf16x3
-    within 0.05 dB of fp32 for the first X3_EPOCHS epochs (200 steps), where
-    the fp32 floor stays below 0.05 dB too; every later gap is printed beside
-    the floor.  Measured (round 3, MI355X): floor <= 0.048 dB for 38 epochs;
-    bf16x3 <= 0.008 dB for 28 epochs, then 0.1-1 dB (the dW pass's bf16
-    operands); bf16 past 0.05 dB from epoch 22."""
+    pass run in one range instead of two pipelined ones); every gap is
+    printed beside the floor.  Asserted: bf16x3 within 0.05 dB of fp32 over the floor's
+    whole horizon (the epochs before two fp32 orders first differ by more
+    than 0.05 dB).  Round 3 (bf16 dW operands): bf16x3 <= 0.008 dB for 28
+    epochs, then 0.1-1 dB; the CPU/GPU emulation (tools/split_emu.py many,
+    profiles/r04_split_emu_many.md) traced that to the dW pass's bf16 X
+    operands, and the bf16x3 training forward now stores their lo parts
+    (dw.hip DwBody<..., LO>)."""
     root = _data(tmp_path)
     iters = LONG_EPOCHS * N_OBJ
     runs = {}
@@ -132,8 +133,8 @@ def test_many_objects_long_horizon_vs_fp32(tmp_path):
     cross16 = int(np.argmax(gap["bf16"] > 0.05)) if (gap["bf16"] > 0.05).any() else LONG_EPOCHS
     print(f"bf16 first epoch past 0.05 dB: {cross16}")
     assert em["fp32"][-1] > em["fp32"][0] + 3.0        # the run is learning
-    assert floor[:X3_EPOCHS].max() <= 0.05             # two fp32 orders agree over the asserted window
-    assert gap["bf16x3"][:X3_EPOCHS].max() <= 0.05
+    assert horizon >= 20                               # two fp32 orders agree long enough to mean something
+    assert gap["bf16x3"][:horizon].max() <= 0.05
 
 
 @pytest.mark.timeout(600)

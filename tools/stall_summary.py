@@ -20,9 +20,13 @@ def load(d):
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             m = re.search(r"chain_kernel<(\d), \d, \d, (true|false), (\d+), (\d)>", r["Kernel_Name"])
-            if not m:
+            d = re.search(r"\bdw_kernel<(\d)>", r["Kernel_Name"])
+            if m:
+                k = f"chain<P{m.group(1)},{'bwd' if m.group(2) == 'true' else 'fwd'},{m.group(3)}w,mode{m.group(4)}>"
+            elif d:
+                k = f"dw_kernel<P{d.group(1)}>"
+            else:
                 continue
-            k = f"chain<P{m.group(1)},{'bwd' if m.group(2) == 'true' else 'fwd'},{m.group(3)}w,mode{m.group(4)}>"
             out[k][r["Counter_Name"]].append((int(r["Dispatch_Id"]), float(r["Counter_Value"]), int(r["Grid_Size"]),
                                               int(r["Workgroup_Size"])))
     return out
