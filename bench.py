@@ -65,9 +65,11 @@ def parse():
     ap.add_argument("--precision", default="bf16", choices=["bf16", "bf16x3", "fp32"],
                     help="chain arithmetic: bf16 operands | bf16x3 (hi + lo operands, 3 MFMAs per block) | fp32")
     ap.add_argument("--objects", type=int, default=64)
-    ap.add_argument("--weights", default=None,
+    ap.add_argument("--weights", default="weights/c2_regime_400.pth",
                     help="reference-format checkpoint (models.pth: model_params, shape/texture_code_params) to "
-                         "start from instead of random-init weights (tools/make_bench_weights.py); 'none' = random init")
+                         "start from (default: 400 steps of the srncar regime, tools/make_bench_weights.py -- the "
+                         "step measured 1.3%% slower on them than on random-init weights, profiles/r04b_clock.md); "
+                         "'none' = random init")
     # other BASELINE configs, measured for DESIGN.md (the driver runs c2):
     #   c4: optimize.py test-time code optimisation, 50 views x 128^2 x 64
     #       samples per step, fwd + dX only (no weight gradients), bf16
