@@ -132,26 +132,18 @@ template <class E>
 CN_DEV __amdgpu_buffer_rsrc_t slab_rsrc(const void* plane, int F, int wglob, bool live = true) {
   return mkrsrc((const char*)plane + (size_t)wglob * (size_t)F * 32u * sizeof(E), live);
 }
-// bf16: groups 2gp and 2gp+1 of feature tile t (this lane: 4 + 4 features as
-// packed pairs) -> one 16-B store per lane.  v_permlane32_swap exchanges the
-// upper half's group-2gp dwords with the lower half's group-(2gp+1) dwords, so
-// lane s holds features 16gp .. 16gp+7 and lane s+32 features 16gp+8 .. +15 of
-// sample s, which is the bf16 pair-block layout (cn_layout.h); voff16 =
-// bf16_pos(s, gp, h) * 16 + gp * 1024.
-//
-// Hazard (observed on gfx950, ROCm 7.2, not flagged by the compiler): a
-// buffer store whose data comes straight from v_permlane32_swap reads its
-// first data dword late, after the NEXT VALU instruction has already
-// rewritten that register.  The data therefore passes through an asm
-// barrier with wait states before the store, and stays live through a second
-// one after it, so no VALU can reuse those registers inside the window.
-CN_DEV void plane_store_pair(__amdgpu_buffer_rsrc_t r, uint32_t voff16, int t, u32x2 a, u32x2 b) {
-  const auto x = __builtin_amdgcn_permlane32_swap(a[0], b[0], false, false);
-  const auto y = __builtin_amdgcn_permlane32_swap(a[1], b[1], false, false);
-  u32x4 d = u32x4{x[0], y[0], x[1], y[1]};
-  asm volatile("s_nop 3" : "+v"(d));
-  bstore128(r, voff16, d, t * 2048);
-  asm volatile("s_nop 1" ::"v"(d) : "memory");
+// bf16: groups 2gp and 2gp+1 of feature tile t (this lane: features 16gp +
+// 4h .. +3 in a, 16gp + 8 + 4h .. +3 in b, as packed pairs) -> two 8-B stores
+// at their places in the bf16 pair-block layout (cn_layout.h: voff[2gp] /
+// voff[2gp + 1] = slab_off of those features).  Each store instruction still
+// writes one contiguous 512 B (32 positions x 16 B, both lane halves), and
+// the operand registers are stored as they are: no lane exchange, so no
+// register copies, and none of the wait states a store fed by
+// v_permlane32_swap needed on gfx950 (its first data dword was read after
+// the next VALU had rewritten it -- round 3's 16-B store path).
+CN_DEV void plane_store_pair(__amdgpu_buffer_rsrc_t r, uint32_t voffa, uint32_t voffb, int t, u32x2 a, u32x2 b) {
+  bstore64(r, voffa, a, t * 2048);
+  bstore64(r, voffb, b, t * 2048);
 }
 
 template <int P, int SB, int TB, bool BWD, int WAVES, int MODE>
@@ -244,12 +236,12 @@ struct Chain {
     const Layer l = S::L(i);
     if (!BWD) {
       int s = 0;
-      if (plane_of(i) && !defers(i)) s += l.T * (kBf16 ? 2 : 4);
+      if (plane_of(i) && !defers(i)) s += l.T * 4;     // 4 stores per tile (bf16: 2 pairs x 2)
       if (TRAIN && l.mask >= 0) s += 1;
       if (l.epi == EPI_SHAPE) s += TRAIN ? 2 : 1;
       return s;   // EPI_RGB stores come after the last wait: not counted (safe)
     }
-    return plane_of(i) && !defers(i) ? l.T * (kBf16 ? 2 : 4) : 0;
+    return plane_of(i) && !defers(i) ? l.T * 4 : 0;
   }
   // ---------------- epilogue schedule (see the epilogues below)
   // layers whose epilogue is spread over the next layer's first tile
@@ -294,7 +286,7 @@ struct Chain {
       if (!diag(i) && S::last_block(i) == g) s += stores_of_layer(i);
       if (diag(i) && final_block(i) == g) s += final_stores(i);
     }
-    if (deferred_at(g) >= 0) s += kXlo ? 2 : 1;
+    if (deferred_at(g) >= 0) s += kXlo ? 4 : 2;     // one (or, with the lo plane, two) pair stores
     return s;
   }
   static constexpr int stores_between(int b0, int b1) {
@@ -362,11 +354,9 @@ struct Chain {
     const int mc = m < a.M ? m : a.M - 1;
     const int wglob = blockIdx.x * WAVES + w;
     float* prm = (float*)(smem + kRingBytes);
-    uint32_t voff[6];   // [g]: 8-B stores of group g; [4 + gp]: bf16 16-B pair stores
+    uint32_t voff[4];   // [g]: the 8-B (bf16) / 16-B (fp32) stores of feature group g
 #pragma unroll
     for (int g = 0; g < 4; ++g) voff[g] = (uint32_t)slab_off(lane & 31, 8 * g + 4 * h, (int)sizeof(E));
-#pragma unroll
-    for (int gp = 0; gp < 2; ++gp) voff[4 + gp] = (uint32_t)(bf16_pos(lane & 31, gp, h) * 16 + gp * 1024);
 
     // -- per-call bias blob -> LDS (plain loads; nothing is in flight yet)
     for (int i = threadIdx.x; i < kBlobFloats / 4; i += WAVES * 64)
@@ -496,11 +486,13 @@ struct Chain {
         constexpr int plane = S::L(pl).plane;
         constexpr int F = BWD ? N::dplane_width(plane) : N::plane_width(plane);
         const u32x4 b = bin[j];                    // tile j / 2, pair j % 2
-        plane_store_pair(slab_rsrc<E>(BWD ? a.dA[plane] : a.Y[plane], F, wglob), voff[4 + (j & 1)], j >> 1,
+        plane_store_pair(slab_rsrc<E>(BWD ? a.dA[plane] : a.Y[plane], F, wglob), voff[2 * (j & 1)],
+                         voff[2 * (j & 1) + 1], j >> 1,
                          u32x2{b[0], b[1]}, u32x2{b[2], b[3]});
         if constexpr (kXlo) {
           const u32x4 bl = binl[j];
-          plane_store_pair(slab_rsrc<E>(a.Ylo[plane], F, wglob), voff[4 + (j & 1)], j >> 1, u32x2{bl[0], bl[1]},
+          plane_store_pair(slab_rsrc<E>(a.Ylo[plane], F, wglob), voff[2 * (j & 1)], voff[2 * (j & 1) + 1], j >> 1,
+                           u32x2{bl[0], bl[1]},
                            u32x2{bl[2], bl[3]});
         }
       }
@@ -760,7 +752,7 @@ struct Chain {
         }
         pg[g] = u32x2{p0, p1};
         if constexpr (plane_of(LI) && !defers(LI))
-          if (g & 1) plane_store_pair(ry, voff[4 + (g >> 1)], t, pg[g - 1], pg[g]);
+          if (g & 1) plane_store_pair(ry, voff[g - 1], voff[g], t, pg[g - 1], pg[g]);
       } else {
         if constexpr (l.epi == EPI_RELU) {
           v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
@@ -893,7 +885,7 @@ struct Chain {
         }
         pg[g] = u32x2{p0, p1};
         if constexpr (plane_of(LI) && !defers(LI))
-          if (g & 1) plane_store_pair(rdA, voff[4 + (g >> 1)], t, pg[g - 1], pg[g]);
+          if (g & 1) plane_store_pair(rdA, voff[g - 1], voff[g], t, pg[g - 1], pg[g]);
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i) bin[16 * t + 4 * g + i] = v[i];
