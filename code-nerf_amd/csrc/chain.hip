@@ -309,37 +309,17 @@ struct Chain {
       if (wp(c) == g) return c;
     return -1;
   }
-  // Staggered weight stream (8-wave workgroups, two waves per SIMD): waves
-  // w and w + 4 share a SIMD (a workgroup's waves are placed on the SIMDs
-  // cyclically), so waves 4..7 issue their LDS-DMA pieces of chunk c + D
-  // kLateOff blocks after chunk c's wait point instead of right after its
-  // barrier -- the two waves of a SIMD then never stall on DMA issue at the
-  // same time and one keeps the matrix pipe fed.  Still safe: the refilled
-  // slot (chunk c - 2's) stays free until the next barrier at least.
-  // (the dX chain only: the 8-wave forward sits at the 256-register limit,
-  // and the issue branches pushed it into scratch)
-  static constexpr bool kStagger = WAVES == 8 && kBf16 && BWD;
-  static constexpr int kLateOff = kChunkBlocks / 2;
-  static constexpr int lp(int c) { return wp(c) + kLateOff; }   // late issue point of chunk c + D
-  static constexpr int late_chunk_at(int g) {
-    for (int c = 0; c < kChunks; ++c)
-      if (c + D < kChunks && lp(c) == g) return c;
-    return -1;
-  }
   // Younger VMEM ops that may still be in flight at chunk c's wait point:
-  // the LDS-DMAs issued after chunk c's and the stores issued since it (an
-  // issue point's DMAs go out before that block's stores).  late: the
-  // counts of a wave that issues at lp() instead of wp().
-  static constexpr int vm_wait(int c, bool late = false) {
-    auto at = [&](int w) { return late ? lp(w) : wp(w); };
+  // the LDS-DMAs issued after chunk c's and the stores issued since it.
+  static constexpr int vm_wait(int c) {
     int n = 0;
     if (c < D) {
       for (int i = c + 1; i < D; ++i) n += issued(i);        // the initial issue, younger than c
-      for (int w = 0; w + D < kChunks && at(w) < wp(c); ++w) n += issued(w + D);
+      for (int w = 0; w < c; ++w) n += issued(w + D);        // wait points 0 .. c-1
       n += stores_between(0, wp(c));
     } else {
-      for (int w = c - D + 1; w + D < kChunks && at(w) < wp(c); ++w) n += issued(w + D);
-      n += stores_between(at(c - D), wp(c));
+      for (int w = c - D + 1; w < c; ++w) n += issued(w + D);
+      n += stores_between(wp(c - D), wp(c));
     }
     return n;
   }
@@ -410,24 +390,13 @@ struct Chain {
       constexpr int g = gc;
       constexpr int wc = wait_chunk_at(g);
       if constexpr (wc >= 0) {
-        // a late wave has fewer younger VMEM ops in flight than an early
-        // one (its DMA went out after some of the stores): its count serves
-        // both (an early wave then also waits for stores >= 2 chunks old)
-        wait_vmcnt<vm_wait(wc, kStagger)>();
+        wait_vmcnt<vm_wait(wc)>();
         block_barrier_noread();
-        if constexpr (wc + D < kChunks) {
-          if (!kStagger || w < 4) issue<wc + D>(a, smem, w, lane);
-        }
+        if constexpr (wc + D < kChunks) issue<wc + D>(a, smem, w, lane);
         if constexpr (wc == 0 && kBf16)
           static_for<0, kPF>([&](auto bb) {
             if constexpr (bb < S::kBlocks) aread(bb);
           });
-      }
-      if constexpr (kStagger) {
-        constexpr int lc = late_chunk_at(g);
-        if constexpr (lc >= 0) {
-          if (w >= 4) issue<lc + D>(a, smem, w, lane);
-        }
       }
       constexpr int li = S::layer_of(g);
       constexpr int lb = g - S::first_block(li);

@@ -78,9 +78,14 @@ struct DwBody {
   // slab itself, as many slots (<= 4) as fit beside the padding pieces
   static constexpr int kLoRing = (kDwSmem - (8 * kG - kPieces) * 1024) / (kPieces * 1024);
   static constexpr int kDwSlot = LO ? kPieces * 1024 : kBf16 ? (KIND == DW_FULL ? 32 * 1024 : 36 * 1024) : 72 * 1024;
-  static constexpr int kDwRing = LO ? (kLoRing < 4 ? kLoRing : 4) : kBf16 ? 4 : 2;
+  // Paired staging (the bf16 256 x 256 bodies): one barrier and one 64 KiB
+  // DMA batch per TWO slabs over a 5-slot ring (three slabs in flight while
+  // two are consumed) -- the LO bodies' 48 KiB batches streamed at 6.2 TB/s
+  // where per-slab 32 KiB batches stream at 5.5 (profiles/r04c, r04e)
+  static constexpr bool kPair = kBf16 && !LO && KIND == DW_FULL;
+  static constexpr int kDwRing = kPair ? 5 : LO ? (kLoRing < 4 ? kLoRing : 4) : kBf16 ? 4 : 2;
   static_assert(!LO || kDwRing >= 3, "a LO slab must leave a 3-slot ring");
-  static constexpr int kDwDepth = kDwRing - 1;        // slabs in flight while one is consumed
+  static constexpr int kDwDepth = kPair ? 3 : kDwRing - 1;   // slabs issued before the first barrier
   static constexpr int kDwDummy = kDwRing * kDwSlot;  // landing area of padding pieces
   static_assert(kPieces * 1024 <= kDwSlot, "dw stage");
   static_assert(kDwDummy + (8 * kG - kPieces) * 1024 <= kDwSmem, "dw LDS");
@@ -172,12 +177,25 @@ struct DwBody {
 
     auto body = [&](int st, auto slotc) {
       constexpr int SL = decltype(slotc)::value;
-      const int ahead = min(kDwDepth - 1, nst - 1 - st);
-      static_for<0, kDwDepth>([&](auto n) {
-        if (n == ahead) wait_vmcnt<n * kG>();
-      });
-      block_barrier();
-      if (st + kDwDepth < nst) issue(st + kDwDepth, std::integral_constant<int, (SL + kDwDepth) % kDwRing>{});
+      if constexpr (kPair) {
+        // even slab: slabs st and st + 1 must have landed (only st + 2 may
+        // still be in flight); then st + 3 and st + 4 go into the slots of
+        // st - 2 and st - 1, which every wave finished before this barrier
+        if ((st & 1) == 0) {
+          if (st + 2 < nst) wait_vmcnt<kG>();
+          else wait_vmcnt<0>();
+          block_barrier();
+          if (st + 3 < nst) issue(st + 3, std::integral_constant<int, (SL + 3) % kDwRing>{});
+          if (st + 4 < nst) issue(st + 4, std::integral_constant<int, (SL + 4) % kDwRing>{});
+        }
+      } else {
+        const int ahead = min(kDwDepth - 1, nst - 1 - st);
+        static_for<0, kDwDepth>([&](auto n) {
+          if (n == ahead) wait_vmcnt<n * kG>();
+        });
+        block_barrier();
+        if (st + kDwDepth < nst) issue(st + kDwDepth, std::integral_constant<int, (SL + kDwDepth) % kDwRing>{});
+      }
       const char* A = smem + SL * kDwSlot;
       const char* X = A + kA * TB;
       const char* Xl = X + (kX0 + kX1) * TB;     // LO: X0's lo tiles

@@ -145,25 +145,33 @@ def _epoch_means(r):
 
 @pytest.mark.timeout(900)
 def test_fine_regime_long_horizon_vs_fp32(tmp_path):
-    """LONG_EPOCHS epochs of the 64 + 64 regime, HIP only: bf16x3 within
-    0.05 dB of HIP fp32 (epoch means) for as long as two fp32 summation
-    orders agree within 0.05 dB (the fp32 floor's horizon); bf16 printed."""
+    """LONG_EPOCHS epochs of the 64 + 64 regime, HIP only, two
+    initialisations: bf16x3 within 0.05 dB of HIP fp32 (epoch means) over
+    the chaos horizon (test_gpu_regime.chaos_horizon: while two fp32
+    summation orders agree within half the bar); bf16 printed."""
+    from test_gpu_regime import chaos_horizon, FLOOR_DB
     root = _data(tmp_path)
     iters = LONG_EPOCHS * N_OBJ
-    runs = {}
-    runs["fp32"], init = _run(tmp_path, root, "fp32", iters)
-    runs["fp32_order"], _ = _run(tmp_path, root, "fp32", iters, init, overlap=False)
-    for prec in ("bf16", "bf16x3"):
-        runs[prec], _ = _run(tmp_path, root, prec, iters, init)
-    em = {k: _epoch_means(v) for k, v in runs.items()}
-    gap = {k: np.abs(v - em["fp32"]) for k, v in em.items()}
-    floor = gap["fp32_order"]
-    horizon = int(np.argmax(floor > BAR_DB)) if (floor > BAR_DB).any() else LONG_EPOCHS
-    print(f"\nepoch-mean fine train PSNR (fp32) {np.round(em['fp32'], 3).tolist()}")
-    for k in ("fp32_order", "bf16", "bf16x3"):
-        print(f"|{k} - fp32| per epoch {np.round(gap[k], 4).tolist()}")
-    print(f"fp32 floor horizon (<= {BAR_DB} dB): {horizon} of {LONG_EPOCHS} epochs; max gap within it: "
-          f"bf16 {gap['bf16'][:horizon].max():.4f}, bf16x3 {gap['bf16x3'][:horizon].max():.4f} dB")
-    assert em["fp32"][-1] > em["fp32"][0] + 3.0          # the run is learning
-    assert horizon >= 10
-    assert gap["bf16x3"][:horizon].max() <= BAR_DB
+    bad = []
+    for seed in (0, 1):
+        runs = {}
+        runs["fp32"], init = _run(tmp_path, root, "fp32", iters, seed=seed)
+        runs["fp32_order"], _ = _run(tmp_path, root, "fp32", iters, init, seed=seed, overlap=False)
+        for prec in ("bf16", "bf16x3"):
+            runs[prec], _ = _run(tmp_path, root, prec, iters, init, seed=seed)
+        em = {k: _epoch_means(v) for k, v in runs.items()}
+        gap = {k: np.abs(v - em["fp32"]) for k, v in em.items()}
+        horizon = chaos_horizon(gap["fp32_order"], LONG_EPOCHS)
+        print(f"\nseed {seed}: epoch-mean fine train PSNR (fp32) {np.round(em['fp32'], 3).tolist()}")
+        for k in ("fp32_order", "bf16", "bf16x3"):
+            print(f"seed {seed}: |{k} - fp32| per epoch {np.round(gap[k], 4).tolist()}")
+        first = {k: (int(np.argmax(gap[k] > BAR_DB)) if (gap[k] > BAR_DB).any() else None) for k in gap}
+        print(f"seed {seed}: chaos horizon (fp32 floor <= {FLOOR_DB} dB) {horizon} of {LONG_EPOCHS} epochs; max gap "
+              f"within it: bf16 {gap['bf16'][:horizon].max():.4f}, bf16x3 {gap['bf16x3'][:horizon].max():.4f} dB; "
+              f"first epoch past {BAR_DB} dB: floor {first['fp32_order']}, bf16 {first['bf16']}, "
+              f"bf16x3 {first['bf16x3']}")
+        assert em["fp32"][-1] > em["fp32"][0] + 3.0          # the run is learning
+        assert horizon >= 10
+        if gap["bf16x3"][:horizon].max() > BAR_DB:
+            bad.append((seed, horizon, float(gap["bf16x3"][:horizon].max())))
+    assert not bad, bad
