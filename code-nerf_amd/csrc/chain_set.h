@@ -116,6 +116,20 @@ constexpr size_t dw_part_bytes() {
   return (size_t)kDwWorkgroups * 2 * ((size_t)kPartRows * kPartCols + kPartRows) * sizeof(float);
 }
 
+// The schedule's unit is a slab's COST (DwArgs::wprefix / pbytes).  bf16 dW
+// is HBM-bound: cost = operand bytes.  The exact-fp32 pass is MFMA-bound and
+// its bodies differ 16x in MFMAs per byte (DW_VIEWDIR 1,280 v_mfma_f32_32x32x2
+// per 72 KiB slab, DW_RGB2 64 per 20 KiB), so equal byte shares left the
+// workgroups holding viewdir / 256x256 slabs ~1.25x the mean while the
+// others idled: cost = CU cycles, max(MFMA cycles over 4 SIMDs -- 64 per
+// MFMA --, bytes at ~9 B per CU-cycle of HBM) + a barrier's ~512.
+constexpr int dw_f32_slab_cost(int kind, int bytes) {
+  const int mfma = kind == DW_FULL ? 1024 : kind == DW_PE ? 256 : kind == DW_VIEWDIR ? 1280
+                 : kind == DW_RGB0 ? 512 : 64;                 // per slab, all waves (dw.hip DwShape)
+  const int mc = mfma * 16, bc = bytes / 9;
+  return (mc > bc ? mc : bc) + 512;
+}
+
 template <int P, int SB, int TB>
 size_t dw_ws_bytes(int) {
   return dw_part_bytes() + (size_t)kFoldRows * kFoldCols * sizeof(float);   // + the fold operand Gx
@@ -178,6 +192,7 @@ int dw_setup(char* act, int act_M, int row0, int M, int nwg_req, const float* zv
       if (p.a_tiles != e[0] || p.x0_tiles != e[1] || p.x1_tiles != e[2] || p.out_tiles != e[3]) return -1;
     }
     dw->pbytes[k] = (p.a_tiles + p.x0_tiles * (1 + p.lo) + p.x1_tiles) * 1024 * ES;
+    if constexpr (P == CN_P_FP32) dw->pbytes[k] = dw_f32_slab_cost(p.kind, dw->pbytes[k]);
     dw->wprefix[k] = wsum;
     const long long tot = (long long)dw->pbytes[k] * dw->total_tiles;
     wsum += tot;

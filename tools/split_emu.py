@@ -53,6 +53,11 @@ VARIANTS = {
     "s3_dwdy": dict(ops=dict(fw_w=S, fw_x=S, bw_w=S, bw_dy=S, dw_dy=S)),
     "s3_dwx": dict(ops=dict(fw_w=S, fw_x=S, bw_w=S, bw_dy=S, dw_x=S)),
     "s3_dwall": dict(ops=dict(fw_w=S, fw_x=S, bw_w=S, bw_dy=S, dw_x=S, dw_dy=S)),
+    # weights plain bf16 (no W lo stream, 2 MFMAs per block: W_hi x_hi + W_hi x_lo),
+    # chain operands split, dW X split -- in both chains / forward / dX only
+    "wb_s2": dict(ops=dict(fw_w=B, fw_x=S, bw_w=B, bw_dy=S, dw_x=S)),
+    "wb_fwd": dict(ops=dict(fw_w=B, fw_x=S, bw_w=S, bw_dy=S, dw_x=S)),
+    "wb_bwd": dict(ops=dict(fw_w=S, fw_x=S, bw_w=B, bw_dy=S, dw_x=S)),
     # fp16 operands ("h": one fp16, "hs": fp16 hi + lo) with the backward's
     # gradients scaled by GS (a power of two) before rounding
     "h_all": dict(ops=dict(fw_w="h", fw_x="h", bw_w="h", bw_dy="h", dw_x="h", dw_dy="h", grad_scale=GS)),
