@@ -42,7 +42,7 @@ FLOP_PER_SAMPLE = {"fwd": 899_328, "bwd": 853_248, "dw": 768_256}
 DW_FOLD_FLOP = 2 * 2 * 257 ** 3
 # Bytes per ray-sample the dW pass must read: the bf16 dA + X operand planes
 # the forward / dX chains stored (encoding_shape folded).
-DW_BYTES_PER_SAMPLE = {"bf16": 6_976, "fp32": 13_952}
+DW_BYTES_PER_SAMPLE = {"bf16": 6_976, "bf16x3": 10_432, "fp32": 13_952}   # + the X lo planes in bf16x3
 KERNEL_NAMES = {"fwd": "chain_kernel<fwd,train>", "bwd": "chain_kernel<bwd>", "dw": "dw_kernel"}
 # algorithmic HBM bytes per ray of the fused ray-major step
 # (24 B origin + direction in, 12 B gt, 12 B rgb out)
@@ -390,8 +390,8 @@ def kernel_roofline(k, precision, timers, traffic):
     the other stream's kernel are reported apart under ``contended``):
       fwd / bwd chains -- MFMA-bound: algorithmic FLOPs / time vs the dense
         MFMA peak of the precision;
-      dw -- HBM-bound: the operand-plane bytes it must read / time vs 8 TB/s
-        (its MFMA fraction alongside)."""
+      dw -- bf16 / bf16x3: HBM-bound, the operand-plane bytes it must read /
+        time vs 8 TB/s (its MFMA fraction alongside); fp32: MFMA-bound."""
     peak_tf = FP32_PEAK_TFLOPS if precision == "fp32" else BF16_PEAK_TFLOPS
     t, n, nl = timers.split(k, False)
     basis = f"{nl} uncontended launches, HIP events on the launching stream"
@@ -404,13 +404,20 @@ def kernel_roofline(k, precision, timers, traffic):
     tf = (FLOP_PER_SAMPLE[k] * n + (DW_FOLD_FLOP * nl if k == "dw" else 0)) / sec / 1e12
     out = {"kernel": KERNEL_NAMES[k], "ms_per_launch": round(t / nl, 4), "samples_per_launch": n // nl,
            "basis": basis}
-    if k == "dw":
-        gbs = DW_BYTES_PER_SAMPLE["fp32" if precision == "fp32" else "bf16"] * n / sec / 1e9
+    if k == "dw" and precision != "fp32":
+        gbs = DW_BYTES_PER_SAMPLE[precision] * n / sec / 1e9
         out.update(bound="hbm", achieved=round(gbs, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                   frac=round(gbs / HBM_PEAK_GBS, 4), bytes_per_sample=DW_BYTES_PER_SAMPLE.get(
-                       "fp32" if precision == "fp32" else "bf16"),
+                   frac=round(gbs / HBM_PEAK_GBS, 4), bytes_per_sample=DW_BYTES_PER_SAMPLE[precision],
                    mfma={"achieved": round(tf, 2), "peak": peak_tf, "unit": "TFLOP/s",
                          "frac": round(tf / peak_tf, 4)})
+    elif k == "dw":
+        # the exact-fp32 dW pass is MFMA-bound (16 K SIMD cycles of
+        # v_mfma_f32_32x32x2_f32 per 64 KiB slab): FLOPs first, bytes beside
+        gbs = DW_BYTES_PER_SAMPLE["fp32"] * n / sec / 1e9
+        out.update(bound="mfma", achieved=round(tf, 2), peak=peak_tf, unit="TFLOP/s", frac=round(tf / peak_tf, 4),
+                   flop_per_sample=FLOP_PER_SAMPLE[k],
+                   hbm={"achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_sample": DW_BYTES_PER_SAMPLE["fp32"]})
     else:
         out.update(bound="mfma", achieved=round(tf, 2), peak=peak_tf, unit="TFLOP/s", frac=round(tf / peak_tf, 4),
                    flop_per_sample=FLOP_PER_SAMPLE[k])

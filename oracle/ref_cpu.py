@@ -140,7 +140,12 @@ class _Bf16Linear(torch.autograd.Function):
         gs = o.get("grad_scale", 1.0)
         dx = _q(dy, o["bw_dy"], gs) @ _q(w, o["bw_w"])
         d2 = _q(dy, o["dw_dy"], gs).reshape(-1, dy.shape[-1])
-        x2 = _q(x, o["dw_x"]).reshape(-1, x.shape[-1])
+        n = o.get("dw_x_split_cols")       # the kernels: only the leading n columns split
+        if n is None:
+            x2 = _q(x, o["dw_x"])
+        else:
+            x2 = torch.cat([_q(x[..., :n], o["dw_x"]), _q(x[..., n:], "b")], -1)
+        x2 = x2.reshape(-1, x.shape[-1])
         return dx, d2.t() @ x2, d2.sum(0), None
 
 
@@ -307,10 +312,10 @@ def sample_pdf(sigmas, z_vals, rand):
     z = z_vals.expand(R, Nc) if z_vals.dim() == 1 else z_vals
     w = composite_weights(sig, z)[:, 1:-1] + 1e-5
     cs = torch.cumsum(w.double(), -1)
-    cdf = torch.cat([torch.zeros(R, 1, dtype=torch.float32), (cs / cs[:, -1:]).float()], -1)   # (R, Nc-1)
+    cdf = torch.cat([torch.zeros(R, 1, dtype=torch.float32, device=sig.device), (cs / cs[:, -1:]).float()], -1)   # (R, Nc-1)
     bins = 0.5 * (z[:, :-1] + z[:, 1:])
     Nf = rand.shape[-1]
-    u = (torch.arange(Nf, dtype=torch.float32)[None, :] + rand) / Nf
+    u = (torch.arange(Nf, dtype=torch.float32, device=rand.device)[None, :] + rand) / Nf
     inds = torch.searchsorted(cdf, u.contiguous(), right=True)
     below = torch.clamp(inds - 1, min=0)
     above = torch.clamp(inds, max=Nc - 2)

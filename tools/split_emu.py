@@ -53,6 +53,15 @@ VARIANTS = {
     "s3_dwdy": dict(ops=dict(fw_w=S, fw_x=S, bw_w=S, bw_dy=S, dw_dy=S)),
     "s3_dwx": dict(ops=dict(fw_w=S, fw_x=S, bw_w=S, bw_dy=S, dw_x=S)),
     "s3_dwall": dict(ops=dict(fw_w=S, fw_x=S, bw_w=S, bw_dy=S, dw_x=S, dw_dy=S)),
+    # the built bf16x3 exactly: encoding_viewdir's dir-PE columns stay hi only
+    # in dW (dw.hip: its LO slab would not fit the ring) -- and with the dW
+    # upstream gradients split too
+    "x3_kernel": dict(ops=dict(fw_w=S, fw_x=S, bw_w=S, bw_dy=S, dw_x=S),
+                      layer_ops={"encoding_viewdir.0": dict(fw_w=S, fw_x=S, bw_w=S, bw_dy=S, dw_x=S,
+                                                            dw_x_split_cols=256)}),
+    "x3_kernel_dwall": dict(ops=dict(fw_w=S, fw_x=S, bw_w=S, bw_dy=S, dw_x=S, dw_dy=S),
+                            layer_ops={"encoding_viewdir.0": dict(fw_w=S, fw_x=S, bw_w=S, bw_dy=S, dw_x=S,
+                                                                  dw_dy=S, dw_x_split_cols=256)}),
     # weights plain bf16 (no W lo stream, 2 MFMAs per block: W_hi x_hi + W_hi x_lo),
     # chain operands split, dW X split -- in both chains / forward / dX only
     "wb_s2": dict(ops=dict(fw_w=B, fw_x=S, bw_w=B, bw_dy=S, dw_x=S)),
