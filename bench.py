@@ -111,33 +111,72 @@ def make_pose(radius, az_deg, el_deg):
 
 
 class Timers:
-    """HIP events around the kernels of one phase, on the launching stream."""
+    """Per-kernel timers of the hot launches (chains, dW): two hipEvents per
+    launch, recorded by the launch's own dispatch packet (cn_time_next_launch
+    -> hipExtLaunchKernel) without a system-scope fence, so nothing sits
+    between kernels (torch events around every launch added ~7 us each to the
+    step)."""
 
     def __init__(self):
         self.ev = {}
         self.on = False
+        self._hip = None
+
+    def _rt(self):
+        if self._hip is None:
+            import ctypes
+            h = ctypes.CDLL("libamdhip64.so.7")      # the process's HIP runtime (torch's, same SONAME)
+            h.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+            h.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
+            h.hipEventDestroy.argtypes = [ctypes.c_void_p]
+            h.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+            self._hip = h
+        return self._hip
+
+    def _event(self):
+        import ctypes
+        e = ctypes.c_void_p()
+        # hipEventDisableSystemFence: a timing event needs its timestamp, not
+        # the system-scope release (an L2 write-back) a default event adds
+        if self._rt().hipEventCreateWithFlags(ctypes.byref(e), 0x20000000) != 0:
+            raise RuntimeError("hipEventCreateWithFlags failed")
+        return e
+
+    def record(self, e):
+        """record e on the current stream"""
+        import ctypes
+        if self._rt().hipEventRecord(e, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)) != 0:
+            raise RuntimeError("hipEventRecord failed")
+
+    def _ms(self, a, b):
+        import ctypes
+        ms = ctypes.c_float()
+        if self._rt().hipEventElapsedTime(ctypes.byref(ms), a, b) != 0:
+            raise RuntimeError("hipEventElapsedTime failed")
+        return ms.value
 
     def mark(self, name):
+        """Arm the timer of the next hot launch (the caller launches it next)."""
         if not self.on:
             return None
-        s = torch.cuda.Event(enable_timing=True)
-        s.record()
-        return s
+        from codenerf_amd import _lib
+        s, e = self._event(), self._event()
+        if _lib.lib().cn_time_next_launch(s, e) != 0:
+            raise RuntimeError("cn_time_next_launch failed")
+        return (s, e)
 
     def done(self, name, s, n=0, contended=False):
         """n: samples the launch processed; contended: it shared the chip
         with a launch on another stream (render.ImageStep's dX / dW overlap)."""
         if s is None:
             return
-        e = torch.cuda.Event(enable_timing=True)
-        e.record()
-        self.ev.setdefault(name, []).append((s, e, int(n), bool(contended)))
+        self.ev.setdefault(name, []).append((s[0], s[1], int(n), bool(contended)))
 
     def summary(self):
         """phase -> (mean ms per launch, total ms over the timed steps)"""
         out = {}
         for k, v in self.ev.items():
-            tot = sum(x[0].elapsed_time(x[1]) for x in v)
+            tot = sum(self._ms(x[0], x[1]) for x in v)
             out[k] = (tot / len(v), tot)
         return out
 
@@ -145,7 +184,7 @@ class Timers:
         """(total ms, total samples, launches) over the phase's launches that
         did / did not share the chip"""
         v = [x for x in self.ev.get(name, []) if x[3] == contended]
-        return sum(x[0].elapsed_time(x[1]) for x in v), sum(x[2] for x in v), len(v)
+        return sum(self._ms(x[0], x[1]) for x in v), sum(x[2] for x in v), len(v)
 
 
 def build_workload(args, dev, rank, world, precision, timers, dist):
@@ -277,19 +316,21 @@ def timed_run(wl, steps, warmup, timers, dist, dev):
         dist.barrier()
     torch.cuda.synchronize()
     timers.on = True
-    marks = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    # per-step marks: fence-less events (Timers.record), not torch events,
+    # whose system-scope release would add an L2 write-back to every step
+    marks = [timers._event() for _ in range(steps + 1)]
     t0 = time.perf_counter()
-    marks[0].record()
+    timers.record(marks[0])
     for i in range(steps):
         wl["step"](warmup + i)
-        marks[i + 1].record()
+        timers.record(marks[i + 1])
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     timers.on = False
-    per = sorted(marks[i].elapsed_time(marks[i + 1]) for i in range(steps))
+    per = sorted(timers._ms(marks[i], marks[i + 1]) for i in range(steps))
     median = per[len(per) // 2] if steps % 2 else 0.5 * (per[steps // 2 - 1] + per[steps // 2])
     if dist is not None:
         t = torch.tensor([dt, median], device=dev, dtype=torch.float64)
@@ -394,7 +435,7 @@ def kernel_roofline(k, precision, timers, traffic):
         time vs 8 TB/s (its MFMA fraction alongside); fp32: MFMA-bound."""
     peak_tf = FP32_PEAK_TFLOPS if precision == "fp32" else BF16_PEAK_TFLOPS
     t, n, nl = timers.split(k, False)
-    basis = f"{nl} uncontended launches, HIP events on the launching stream"
+    basis = f"{nl} uncontended launches, HIP events recorded by each launch's dispatch (hipExtLaunchKernel)"
     if n <= 0 or t <= 0:
         t, n, nl = timers.split(k, True)
         basis = f"{nl} launches beside the other stream's kernel (none ran alone)"

@@ -18,7 +18,7 @@ _IN_TREE = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # product path (tests, smoke, bench) always runs the in-tree library.
 LIB_PATH = os.environ.get("CODENERF_LIB") or _IN_TREE
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 CN_FP32 = 0
 CN_BF16 = 1
 CN_BF16X3 = 2
@@ -41,6 +41,8 @@ _Z = ctypes.c_size_t
 _SIGS = {
     "cn_abi_version": (_I, []),
     "cn_last_error": (ctypes.c_char_p, []),
+    "cn_time_next_launch": (_I, [_P, _P]),
+    "cn_stream_wait": (_I, [_P, _P]),
     "cn_plan_create": (_I, [_I, _I, _I, _I, _I, _I, _I, ctypes.POINTER(_P)]),
     "cn_plan_destroy": (None, [_P]),
     "cn_plan_num_params": (_I, [_P]),

@@ -139,8 +139,8 @@ size_t dw_ws_bytes(int) {
 // (row0 a multiple of 256): the coarse and fine row ranges of one step can
 // then be reduced by two launches, each overlapping the other range's dX chain.
 template <int P, int SB, int TB>
-int dw_setup(char* act, int act_M, int row0, int M, int nwg_req, const float* zvec, float* dbuf, char* ws,
-             DwArgs* dw, DwRedArgs* red) {
+int dw_setup_cost(char* act, int act_M, int row0, int M, int nwg_req, const float* zvec, float* dbuf, char* ws,
+                  DwArgs* dw, DwRedArgs* red, bool cost) {
   using N = Net<SB, TB>;
   constexpr ParamIdx PI{SB, TB};
   constexpr int ES = P != CN_P_FP32 ? 2 : 4;
@@ -192,7 +192,7 @@ int dw_setup(char* act, int act_M, int row0, int M, int nwg_req, const float* zv
       if (p.a_tiles != e[0] || p.x0_tiles != e[1] || p.x1_tiles != e[2] || p.out_tiles != e[3]) return -1;
     }
     dw->pbytes[k] = (p.a_tiles + p.x0_tiles * (1 + p.lo) + p.x1_tiles) * 1024 * ES;
-    if constexpr (P == CN_P_FP32) dw->pbytes[k] = dw_f32_slab_cost(p.kind, dw->pbytes[k]);
+    if (cost) dw->pbytes[k] = dw_f32_slab_cost(p.kind, dw->pbytes[k]);
     dw->wprefix[k] = wsum;
     const long long tot = (long long)dw->pbytes[k] * dw->total_tiles;
     wsum += tot;
@@ -253,6 +253,19 @@ int dw_setup(char* act, int act_M, int row0, int M, int nwg_req, const float* zv
   red->dbpart = dw->dbpart;
   red->fold = (float*)(ws + dw_part_bytes());
   return (int)nwg;
+}
+
+// fp32: MFMA-cost shares (dw_f32_slab_cost); a small call whose cost shares
+// cannot satisfy the segment rules above (a share larger than the cheapest
+// problem) falls back to byte shares
+template <int P, int SB, int TB>
+int dw_setup(char* act, int act_M, int row0, int M, int nwg_req, const float* zvec, float* dbuf, char* ws,
+             DwArgs* dw, DwRedArgs* red) {
+  if constexpr (P == CN_P_FP32) {
+    const int n = dw_setup_cost<P, SB, TB>(act, act_M, row0, M, nwg_req, zvec, dbuf, ws, dw, red, true);
+    if (n > 0) return n;
+  }
+  return dw_setup_cost<P, SB, TB>(act, act_M, row0, M, nwg_req, zvec, dbuf, ws, dw, red, false);
 }
 
 // The encoding_shape fold (see Net::stored): the viewdir problem accumulates

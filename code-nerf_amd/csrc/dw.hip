@@ -409,18 +409,20 @@ __global__ __launch_bounds__(256) void dw_reduce_kernel(DwRedArgs a) {
 
 // ---------------------------------------------------------------- fold
 // The encoding_shape fold (chain_set.h fold_args), two small fp32 GEMMs over
-// the reduced Gx (257 x 257), one 32 x 32 output tile per workgroup:
+// the reduced Gx (257 x 257), one 16 x 16 output tile per workgroup:
 //   z = 0: d[W_v y-part ; w_sigma] (257 x 256)  = Gx . Wx_e^T
 //   z = 1: d[W_e | b_e]            (256 x 257)  = Wx_v^T . Gx
 // ~34 M FMAs per dW launch.
 __global__ __launch_bounds__(256) void dw_fold_kernel(DwFoldArgs a) {
-  // the workgroup's whole K = 257 strips of both operands are staged at once
-  // (67 KB of LDS; one load round trip instead of one per 32-wide K step)
-  __shared__ float As[32][kFoldCols + 3];     // [i][k]
-  __shared__ float Bs[kFoldCols][33];         // [k][j]
+  // one 16 x 16 output tile per workgroup (grid 17 x 17 x 2: ~570 live
+  // workgroups, one output per thread -- 32 x 32 tiles left ~160 workgroups
+  // on 256 CUs running 257-long LDS-latency-bound chains: 28 us per fold);
+  // the workgroup's whole K = 257 strips of both operands staged at once
+  __shared__ float As[16][kFoldCols + 3];     // [i][k]
+  __shared__ float Bs[kFoldCols][17];         // [k][j]
   const int z = blockIdx.z;
   const int rows = z == 0 ? kFoldRows : 256, cols = z == 0 ? 256 : kFoldCols;
-  const int i0 = blockIdx.y * 32, j0 = blockIdx.x * 32;
+  const int i0 = blockIdx.y * 16, j0 = blockIdx.x * 16;
   if (i0 >= rows || j0 >= cols) return;
   const float* G = a.fold;
   const float* We = a.params[a.w_shape];
@@ -431,44 +433,40 @@ __global__ __launch_bounds__(256) void dw_fold_kernel(DwFoldArgs a) {
   // consecutive threads read consecutive addresses of each operand
   if (z == 0) {
     // A = Gx rows i0.. (contiguous), B(k, j) = [W_e | b_e][j][k]
-    for (int e = threadIdx.x; e < 32 * kFoldCols; e += 256) {
+    for (int e = threadIdx.x; e < 16 * kFoldCols; e += 256) {
       const int ii = e / kFoldCols, k = e - ii * kFoldCols;
       As[ii][k] = i0 + ii < rows ? G[(size_t)(i0 + ii) * kFoldCols + k] : 0.f;
     }
-    for (int e = threadIdx.x; e < 32 * 256; e += 256) {
+    for (int e = threadIdx.x; e < 16 * 256; e += 256) {
       const int jj = e >> 8, k = e & 255;
       Bs[k][jj] = We[(size_t)(j0 + jj) * 256 + k];
     }
-    if (threadIdx.x < 32) Bs[256][threadIdx.x] = be[j0 + threadIdx.x];
+    if (threadIdx.x < 16) Bs[256][threadIdx.x] = be[j0 + threadIdx.x];
   } else {
     // A(i, k) = [W_v ; w_sigma][k][i] (rows of W_v contiguous in i), B = Gx
-    for (int e = threadIdx.x; e < kFoldRows * 32; e += 256) {
-      const int k = e >> 5, ii = e & 31;
+    for (int e = threadIdx.x; e < kFoldRows * 16; e += 256) {
+      const int k = e >> 4, ii = e & 15;
       As[ii][k] = k < 256 ? Wv[(size_t)k * VC + i0 + ii] : ws[i0 + ii];
       Bs[k][ii] = j0 + ii < cols ? G[(size_t)k * kFoldCols + j0 + ii] : 0.f;
     }
   }
   __syncthreads();
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;   // 16 x 16
+  float acc0 = 0.f, acc1 = 0.f;                             // two FMA chains
 #pragma unroll 8
-  for (int k = 0; k < kFoldCols; ++k) {
-    const float bv = Bs[k][tx];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) acc[r] = __builtin_fmaf(As[ty + 8 * r][k], bv, acc[r]);
+  for (int k = 0; k < 256; k += 2) {
+    acc0 = __builtin_fmaf(As[ty][k], Bs[k][tx], acc0);
+    acc1 = __builtin_fmaf(As[ty][k + 1], Bs[k + 1][tx], acc1);
   }
-  const int j = j0 + tx;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int i = i0 + ty + 8 * r;
-    if (i >= rows || j >= cols) continue;
-    if (z == 0) {
-      if (i < 256) a.grads[a.w_view][i * VC + j] += acc[r];
-      else a.grads[a.w_sigma][j] += acc[r];
-    } else {
-      if (j < 256) a.grads[a.w_shape][i * 256 + j] += acc[r];
-      else a.grads[a.w_shape + 1][i] += acc[r];
-    }
+  const float acc = __builtin_fmaf(As[ty][256], Bs[256][tx], acc0 + acc1);
+  const int i = i0 + ty, j = j0 + tx;
+  if (i >= rows || j >= cols) return;
+  if (z == 0) {
+    if (i < 256) a.grads[a.w_view][i * VC + j] += acc;
+    else a.grads[a.w_sigma][j] += acc;
+  } else {
+    if (j < 256) a.grads[a.w_shape][i * 256 + j] += acc;
+    else a.grads[a.w_shape + 1][i] += acc;
   }
 }
 

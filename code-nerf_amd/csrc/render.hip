@@ -385,12 +385,18 @@ __global__ __launch_bounds__(256) void fine_render_loss_kernel(
   // weights) the two rank computations below need not form a permutation, and
   // an unwritten slot must not scatter through an undefined index.
   for (int p = lane; p < N; p += 64) m_src[wv][p] = -1;
+  // the ray's coarse and fine z staged in LDS (m_dsig is written only by the
+  // backward below): the rank searches' dependent reads then cost LDS, not
+  // global-memory, latency
+  float* zs = m_dsig[wv];
+  for (int i = lane; i < Nc; i += 64) zs[i] = zcr[i];
+  for (int j = lane; j < Nf; j += 64) zs[Nc + j] = zfr[j];
   wave_sync();
   // merged position = own index + number of the other list's samples before it
   for (int i = lane; i < Nc; i += 64) {
-    const float v = zcr[i];
+    const float v = zs[i];
     int lo = 0, hi = Nf;                    // count zf < v
-    while (lo < hi) { const int mid = (lo + hi) >> 1; if (zfr[mid] < v) lo = mid + 1; else hi = mid; }
+    while (lo < hi) { const int mid = (lo + hi) >> 1; if (zs[Nc + mid] < v) lo = mid + 1; else hi = mid; }
     const int p = i + lo;
     const size_t g = (size_t)r * Nc + i;
     m_sig[wv][p] = sig_c[g];
@@ -401,9 +407,9 @@ __global__ __launch_bounds__(256) void fine_render_loss_kernel(
     m_src[wv][p] = i;
   }
   for (int j = lane; j < Nf; j += 64) {
-    const float v = zfr[j];
+    const float v = zs[Nc + j];
     int lo = 0, hi = Nc;                    // count zc <= v
-    while (lo < hi) { const int mid = (lo + hi) >> 1; if (zcr[mid] <= v) lo = mid + 1; else hi = mid; }
+    while (lo < hi) { const int mid = (lo + hi) >> 1; if (zs[mid] <= v) lo = mid + 1; else hi = mid; }
     const int p = j + lo;
     const size_t g = (size_t)r * Nf + j;
     m_sig[wv][p] = sig_f[g];

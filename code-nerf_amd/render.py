@@ -19,10 +19,14 @@ into ``bwd_ranges`` row ranges; the dX chain of range i runs on the current
 stream while the weight-gradient pass of range i-1 runs on a side stream
 (the dX chain is MFMA-bound, dW streams its operand planes from HBM).
 """
+import ctypes
+
 import torch
 
+from . import _lib
 from . import dp as _dp
 from . import engine as _eng
+from ._lib import check
 
 
 class ImageStep:
@@ -151,17 +155,28 @@ class ImageStep:
             return
         main = torch.cuda.current_stream(eng.device)
         side = self.side_stream(eng.device)
+        L = _lib.lib()
+
+        def wait(waiter, signaller):
+            # fence-less stream dependency (cn_stream_wait): a torch event's
+            # record does a system-scope release -- an L2 write-back of the
+            # planes the last kernel wrote, ~15 us of idle GPU per fork / join
+            check(L.cn_stream_wait(ctypes.c_void_p(waiter.cuda_stream), ctypes.c_void_p(signaller.cuda_stream)),
+                  "cn_stream_wait")
+
         bwd(*ranges[0])
-        for i in range(1, k + 1):
-            ready = torch.cuda.Event()
-            ready.record(main)
-            side.wait_event(ready)
+        for i in range(1, k):
+            wait(side, main)
             with torch.cuda.stream(side):
-                # the last range's dW runs alone: every CU
-                dw(*ranges[i - 1], i - 1, self.dw_side_wgs if i < k else 0, ov=i < k)
-            if i < k:
-                bwd(*ranges[i], ov=True)
-        main.wait_stream(side)
+                dw(*ranges[i - 1], i - 1, self.dw_side_wgs, ov=True)
+            bwd(*ranges[i], ov=True)
+        # the last range's dW runs alone (every CU) on the main stream, right
+        # behind its dX chain: the side stream's dW (which shares the partial
+        # workspace) finished during that chain, so the join is free, where
+        # handing the last dW to the side stream and joining after it added a
+        # second cross-stream dependency per step
+        wait(main, side)
+        dw(*ranges[k - 1], k - 1, 0)
 
     # ------------------------------------------------------------ steps
     def forward_backward(self, rays_o, viewdirs, z_vals, gt, shape_table, texture_table, obj_idx,

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define CN_ABI_VERSION 2
+#define CN_ABI_VERSION 3
 #define CN_FP32 0 /* exact-fp32 MFMA path (parity) */
 #define CN_BF16 1 /* bf16 operands, fp32 accumulate (throughput) */
 /* error-compensated bf16: weights and chain operands as bf16 hi + lo pairs,
@@ -49,6 +49,21 @@ typedef struct cn_plan cn_plan;
 
 int cn_abi_version(void);
 const char *cn_last_error(void);
+
+/* Measurement hook (no reference counterpart; ABI 3): the next chain, dW or
+ * bias-sum kernel the calling thread launches records start_event /
+ * stop_event (hipEvent_t, created by the caller) from its own dispatch
+ * packet (hipExtLaunchKernel), so a per-kernel timer adds no marker packets
+ * between kernels.  Give both or neither (NULL, NULL clears). */
+int cn_time_next_launch(void *start_event, void *stop_event);
+
+/* Stream dependency on one device (ABI 3): `waiter` waits for the work queued
+ * so far on `signaller`, through an event WITHOUT the system-scope fence a
+ * default event record performs (an L2 write-back of everything the last
+ * kernel dirtied: ~15 us behind a chain or dW launch).  For the dX / dW
+ * pipelining of one step (render.ImageStep); host-visible results still need
+ * the stream's own synchronisation. */
+int cn_stream_wait(void *waiter_stream, void *signaller_stream);
 
 /* ---- plan: static layout for one network configuration and precision.
  * Replaces CodeNeRF.__init__ (src/model.py:11-34).  Creating a plan and the

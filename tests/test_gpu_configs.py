@@ -478,5 +478,7 @@ def test_module_forward_over_budget_recomputes_parts(monkeypatch):
         (sig.square().mean() + (rgb * torch.linspace(-1, 1, 3, device=dev)).sum() / B).backward()
         out.append((sig.detach(), rgb.detach(), [p.grad for p in m.parameters()], s.grad, t.grad))
     assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    # fp32 sums over 65 K samples grouped differently (parts; the dW pass's
+    # cost-balanced shares follow the part size): ~sqrt(M) eps = 1.5e-5
     for a, b in zip(out[0][2] + [out[0][3], out[0][4]], out[1][2] + [out[1][3], out[1][4]]):
-        assert _rel_l2(a, b) <= 1e-5
+        assert _rel_l2(a, b) <= 3e-5
