@@ -213,28 +213,33 @@ struct DwBody {
           const int s = 2 * qq + h;
           float fa[NI];
 #pragma unroll
-          for (int i = 0; i < NI; ++i) {
-            fa[i] = val(A, row_tile(w, i), s);
-            if (do_db) dbacc[i] += fa[i];
-          }
+          for (int i = 0; i < NI; ++i) fa[i] = val(A, row_tile(w, i), s);
           float fs = 0.f;
+          if constexpr (kVD) fs = val(A, 8, s);
+          // X values read one column tile ahead of their MFMAs (as the bf16
+          // bodies below)
+          float fx = val(X, col_tile(w, 0), s);
+#pragma unroll
+          for (int i = 0; i < NI; ++i)
+            if (do_db) dbacc[i] += fa[i];
           if constexpr (kVD) {
-            fs = val(A, 8, s);
             if (w == 0) dbsig += fs;
           }
 #pragma unroll
           for (int j = 0; j < NJ; ++j) {
-            const float fx = val(X, col_tile(w, j), s);
+            float nx = 0.f;
+            if (j + 1 < NJ) nx = val(X, col_tile(w, j + 1), s);
+            else if constexpr (kVD) nx = val(X, 8, s);          // the dir-PE input tile
 #pragma unroll
             for (int i = 0; i < NI; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i], fx, acc[i][j], 0, 0, 0);
             if constexpr (kVD) {
               if (j == (w >> 1)) acc_e2 = __builtin_amdgcn_mfma_f32_32x32x2f32(fs, fx, acc_e2, 0, 0, 0);
             }
+            fx = nx;
           }
           if constexpr (kVD) {
-            const float fd = val(X, 8, s);
             const float fr = (w & 1) ? fa[1] : fa[0];
-            acc_e1 = __builtin_amdgcn_mfma_f32_32x32x2f32(fr, fd, acc_e1, 0, 0, 0);
+            acc_e1 = __builtin_amdgcn_mfma_f32_32x32x2f32(fr, fx, acc_e1, 0, 0, 0);   // fx = the dir-PE value
           }
         }
         return;
@@ -242,27 +247,39 @@ struct DwBody {
 #pragma unroll
       for (int kk = 0; kk < 32; kk += 16) {
         const int s = kk + 8 * h + q;
+        // every X fragment is read one column tile ahead of the MFMAs that
+        // use it (the compiler otherwise waits lgkmcnt(0) right behind each
+        // read: the LDS latency stood between every pair of MFMA groups)
         bf16x8 fa[NI];
 #pragma unroll
-        for (int i = 0; i < NI; ++i) {
-          fa[i] = frag(A, row_tile(w, i), s);
-          if (do_db) dbacc[i] += rowsum(fa[i]);
-        }
+        for (int i = 0; i < NI; ++i) fa[i] = frag(A, row_tile(w, i), s);
         bf16x8 fs{};
+        if constexpr (kVD) fs = frag(A, 8, s);   // sigma-head columns 256.. of the dA plane
+        bf16x8 fx = frag(X, col_tile(w, 0), s);
+        bf16x8 fxl{};
+        if constexpr (LO) fxl = frag(Xl, col_tile(w, 0), s);
+        // bias sums (VALU) while the reads are in flight
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+          if (do_db) dbacc[i] += rowsum(fa[i]);
         if constexpr (kVD) {
-          fs = frag(A, 8, s);                    // sigma-head columns 256.. of the dA plane
           if (w == 0) dbsig += rowsum(fs);
         }
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-          const bf16x8 fx = frag(X, col_tile(w, j), s);
+          bf16x8 nx{}, nxl{};
+          if (j + 1 < NJ) {
+            nx = frag(X, col_tile(w, j + 1), s);
+            if constexpr (LO) nxl = frag(Xl, col_tile(w, j + 1), s);
+          } else if constexpr (kVD) {
+            nx = frag(X, 8, s);                  // the dir-PE input tile, for acc_e1 below
+          }
 #pragma unroll
           for (int i = 0; i < NI; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fx, acc[i][j], 0, 0, 0);
           if constexpr (kVD) {
             if (j == (w >> 1)) acc_e2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fs, fx, acc_e2, 0, 0, 0);
           }
           if constexpr (LO) {
-            const bf16x8 fxl = frag(Xl, col_tile(w, j), s);
 #pragma unroll
             for (int i = 0; i < NI; ++i)
               acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fxl, acc[i][j], 0, 0, 0);
@@ -270,11 +287,12 @@ struct DwBody {
               if (j == (w >> 1)) acc_e2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fs, fxl, acc_e2, 0, 0, 0);
             }
           }
+          fx = nx;
+          fxl = nxl;
         }
         if constexpr (kVD) {
-          const bf16x8 fd = frag(X, 8, s);       // dir-PE input tile
           const bf16x8 fr = (w & 1) ? fa[1] : fa[0];
-          acc_e1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr, fd, acc_e1, 0, 0, 0);
+          acc_e1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr, fx, acc_e1, 0, 0, 0);   // fx = the dir-PE tile
         }
       }
     };
@@ -452,13 +470,11 @@ __global__ __launch_bounds__(256) void dw_fold_kernel(DwFoldArgs a) {
   }
   __syncthreads();
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;   // 16 x 16
-  float acc0 = 0.f, acc1 = 0.f;                             // two FMA chains
+  // one FMA chain in k order: the fp32 parity path's sums stay in the order
+  // the trajectory tests were pinned with (tiling changes no sum)
+  float acc = 0.f;
 #pragma unroll 8
-  for (int k = 0; k < 256; k += 2) {
-    acc0 = __builtin_fmaf(As[ty][k], Bs[k][tx], acc0);
-    acc1 = __builtin_fmaf(As[ty][k + 1], Bs[k + 1][tx], acc1);
-  }
-  const float acc = __builtin_fmaf(As[ty][256], Bs[256][tx], acc0 + acc1);
+  for (int k = 0; k < kFoldCols; ++k) acc = __builtin_fmaf(As[ty][k], Bs[k][tx], acc);
   const int i = i0 + ty, j = j0 + tx;
   if (i >= rows || j >= cols) return;
   if (z == 0) {

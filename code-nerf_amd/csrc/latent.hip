@@ -15,25 +15,6 @@
 
 namespace cn {
 
-// row . x over 256 columns, one thread per row: 64 float4 loads walking the
-// row (the row's 128-B lines are re-read from L1 by the next loads), x from LDS
-CN_DEV float row_dot256(const float* row, const float* x) {
-  float s0 = 0.f, s1 = 0.f;
-#pragma unroll 8
-  for (int k = 0; k < 256; k += 8) {
-    const f32x4 v = *(const f32x4*)(row + k), u = *(const f32x4*)(row + k + 4);
-    s0 = __builtin_fmaf(v[0], x[k], s0);
-    s1 = __builtin_fmaf(v[1], x[k + 1], s1);
-    s0 = __builtin_fmaf(v[2], x[k + 2], s0);
-    s1 = __builtin_fmaf(v[3], x[k + 3], s1);
-    s0 = __builtin_fmaf(u[0], x[k + 4], s0);
-    s1 = __builtin_fmaf(u[1], x[k + 5], s1);
-    s0 = __builtin_fmaf(u[2], x[k + 6], s0);
-    s1 = __builtin_fmaf(u[3], x[k + 7], s1);
-  }
-  return s0 + s1;
-}
-
 template <int SB, int TB>
 __global__ __launch_bounds__(256) void latent_fwd_kernel(LatentArgs a) {
   using N = Net<SB, TB>;
@@ -56,13 +37,19 @@ __global__ __launch_bounds__(256) void latent_fwd_kernel(LatentArgs a) {
     const int lw = shape ? P.shape_latent_w(inj) : P.tex_latent_w(inj - SB);
     code[i] = (shape ? a.shape_code : a.texture_code)[i];
     __syncthreads();
-    const float acc = row_dot256(a.params[lw] + (size_t)i * 256, code) + a.params[lw + 1][i];
+    const float* Lw = a.params[lw] + (size_t)i * 256;
+    float acc = 0.f;
+    for (int k = 0; k < 256; ++k) acc = __builtin_fmaf(Lw[k], code[k], acc);
+    acc += a.params[lw + 1][i];
     const float zi = acc > 0.f ? acc : 0.f;
     z[i] = zi;
     a.zvec[inj * 256 + i] = zi;
     __syncthreads();
     // row i of W_j (256 x 256): b'_i = b_i + sum_k W[i][k] z[k]
-    b += row_dot256(a.params[l.w] + (size_t)i * 256, z);
+    const float* W = a.params[l.w] + (size_t)i * 256;
+    float s = 0.f;
+    for (int k = 0; k < 256; ++k) s = __builtin_fmaf(W[k], z[k], s);
+    b += s;
   }
   a.blob[L * 256 + i] = b;
 }
