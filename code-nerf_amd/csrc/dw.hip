@@ -232,14 +232,13 @@ struct DwBody {
             else if constexpr (kVD) nx = val(X, 8, s);          // the dir-PE input tile
 #pragma unroll
             for (int i = 0; i < NI; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i], fx, acc[i][j], 0, 0, 0);
-            if constexpr (kVD) {
-              if (j == (w >> 1)) acc_e2 = __builtin_amdgcn_mfma_f32_32x32x2f32(fs, fx, acc_e2, 0, 0, 0);
-            }
             fx = nx;
           }
           if constexpr (kVD) {
             const float fr = (w & 1) ? fa[1] : fa[0];
             acc_e1 = __builtin_amdgcn_mfma_f32_32x32x2f32(fr, fx, acc_e1, 0, 0, 0);   // fx = the dir-PE value
+            // the sigma-head row against column tile w >> 1 (no branch in the loop)
+            acc_e2 = __builtin_amdgcn_mfma_f32_32x32x2f32(fs, val(X, 4 * (w & 1) + (w >> 1), s), acc_e2, 0, 0, 0);
           }
         }
         return;
@@ -276,7 +275,7 @@ struct DwBody {
           }
 #pragma unroll
           for (int i = 0; i < NI; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fx, acc[i][j], 0, 0, 0);
-          if constexpr (kVD) {
+          if constexpr (kVD && LO) {      // (LO: no registers left for a re-read after the loop)
             if (j == (w >> 1)) acc_e2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fs, fx, acc_e2, 0, 0, 0);
           }
           if constexpr (LO) {
@@ -293,6 +292,11 @@ struct DwBody {
         if constexpr (kVD) {
           const bf16x8 fr = (w & 1) ? fa[1] : fa[0];
           acc_e1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr, fx, acc_e1, 0, 0, 0);   // fx = the dir-PE tile
+          // the sigma-head tile against this wave's column tile w >> 1 of its
+          // half, read once more instead of a wave-uniform branch inside the
+          // unrolled column loop (each branch target cost hazard NOPs)
+          if constexpr (!LO)
+            acc_e2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fs, frag(X, 4 * (w & 1) + (w >> 1), s), acc_e2, 0, 0, 0);
         }
       }
     };
