@@ -13,8 +13,11 @@
 //     ds_read_b64_tr_b16 (conflict-free by the pair-block rotation) feeding
 //     v_mfma_f32_32x32x16_bf16; the sigma head (ds x y_shape) is an extra
 //     MFMA tile of the viewdir body;
-//   fp32 (DwF32): exact fp32 parity path, register-staged double buffer,
-//     ds_read_b32 + v_mfma_f32_32x32x2_f32.
+//   fp32: exact fp32 parity path, 2-slot LDS-DMA ring of 72 KiB slots,
+//     ds_read_b32 + v_mfma_f32_32x32x2_f32; MFMA-bound, so the schedule
+//     balances MFMA cost instead of bytes (chain_set.h dw_f32_slab_cost).
+// Every body reads its X fragments one column tile ahead of the MFMAs that
+// use them (round 4: the LDS latency had sat between the MFMA groups).
 // Bias gradients (row sums of dA) come from the A fragments.  Workgroups write
 // fp32 partials; dw_reduce sums them (deterministic, no atomics), maps padded /
 // permuted columns back to the reference tensors, adds the code-injection
