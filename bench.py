@@ -564,13 +564,14 @@ def cpu_quota():
 
 
 def cpu_baseline(threads, args):
-    """The oracle sample below at the box's thread counts: the process's
-    OMP_NUM_THREADS share (16 on the GPU box), the cgroup CPU quota, the CPUs
-    it may run on (sched_getaffinity) and every host CPU (os.cpu_count()).
-    Each count runs in a child process with a wall-clock limit, so a count
-    far above the quota (the box: 256 host CPUs, a 16-CPU share) cannot stall
-    the bench; a count that does not finish is listed as such.  ``value`` /
-    ``cores`` are the fastest finished count, every count under ``by_threads``."""
+    """The oracle sample below at the thread counts this process may use: its
+    OMP_NUM_THREADS share (16 on the GPU box), the cgroup CPU quota and the
+    CPUs it may run on (sched_getaffinity), each at most min(quota,
+    affinity).  ``host_cpus`` (os.cpu_count()) is the machine's count, which
+    the process is NOT granted on the box (256 CPUs under a 16-CPU quota) and
+    is not run.  Each count runs in a child process with a wall-clock limit;
+    a count that does not finish is listed as such.  ``value`` / ``cores`` are
+    the fastest finished count, every count under ``by_threads``."""
     if threads is not None:
         return _cpu_baseline_at(threads, args, 10.0)
     omp = int(os.environ.get("OMP_NUM_THREADS", "0")) or None
@@ -579,7 +580,11 @@ def cpu_baseline(threads, args):
     except (AttributeError, OSError):
         aff = None
     quota = cpu_quota()
-    counts = sorted({c for c in (omp, quota, aff, os.cpu_count()) if c})
+    # only counts the process may actually use: a thread count above the
+    # cgroup quota / affinity (the box: 256 host CPUs on a 16-CPU share)
+    # measures oversubscription, not the CPU
+    usable = min([c for c in (quota, aff) if c] or [os.cpu_count() or 1])
+    counts = sorted({c for c in (omp, quota, aff) if c and c <= usable} or {usable})
     runs, by = [], {}
     for c in counts:
         log(f"cpu baseline, {c} threads (child process, limit 90 s)")
@@ -595,6 +600,7 @@ def cpu_baseline(threads, args):
     best["by_threads"] = by
     best["affinity_cpus"] = aff
     best["cgroup_cpu_quota"] = quota
+    best["usable_cpus"] = usable
     best["omp_num_threads"] = omp
     return best
 

@@ -58,6 +58,13 @@ void launch_hot(K kernel, dim3 grid, dim3 block, hipStream_t s, A... args) {
     hipLaunchKernelGGL(kernel, grid, block, 0, s, args...);
   }
 }
+// Armed events belong to the NEXT hot entry call only: every entry point that
+// may launch a hot kernel holds one of these, so an error return, a call with
+// nothing to launch (cn_mlp_dbias without injections) or a failed dW setup
+// disarms them instead of leaving them for an unrelated later launch.
+struct HotCallScope {
+  ~HotCallScope() { g_ev_start = g_ev_stop = nullptr; }
+};
 }  // namespace
 
 extern "C" {
@@ -66,16 +73,33 @@ int cn_abi_version(void) { return CN_ABI_VERSION; }
 const char* cn_last_error(void) { return g_err.c_str(); }
 
 int cn_stream_wait(void* waiter, void* signaller) {
-  // a ring of fence-less events per thread: hipStreamWaitEvent captures the
-  // event's current record, so reusing one 16 records later is safe
-  thread_local hipEvent_t ring[16] = {};
-  thread_local int next = 0;
-  hipEvent_t& e = ring[next];
-  next = (next + 1) % 16;
-  if (!e && check(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence),
-                  "cn_stream_wait: hipEventCreateWithFlags")) {
-    e = nullptr;
+  // a ring of fence-less events per thread AND per device (an event must be
+  // recorded on a stream of the device it was created on): hipStreamWaitEvent
+  // captures the event's current record, so reusing one 16 records later is
+  // safe.  The event is created with the signaller's device current.
+  constexpr int kRing = 16, kDevs = 64;
+  thread_local hipEvent_t ring[kDevs][kRing] = {};
+  thread_local int next[kDevs] = {};
+  hipDevice_t dev = 0;
+  if (signaller) {
+    if (check(hipStreamGetDevice(S(signaller), &dev), "cn_stream_wait: hipStreamGetDevice")) return -1;
+  } else if (check(hipGetDevice(&dev), "cn_stream_wait: hipGetDevice")) {
     return -1;
+  }
+  if (dev < 0 || dev >= kDevs) return fail("cn_stream_wait: device index out of range");
+  hipEvent_t& e = ring[dev][next[dev]];
+  next[dev] = (next[dev] + 1) % kRing;
+  if (!e) {
+    int cur = 0;
+    if (check(hipGetDevice(&cur), "cn_stream_wait: hipGetDevice")) return -1;
+    if (cur != dev && check(hipSetDevice(dev), "cn_stream_wait: hipSetDevice")) return -1;
+    const int rc = check(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence),
+                         "cn_stream_wait: hipEventCreateWithFlags");
+    if (cur != dev) (void)hipSetDevice(cur);
+    if (rc) {
+      e = nullptr;
+      return -1;
+    }
   }
   if (check(hipEventRecord(e, S(signaller)), "cn_stream_wait: hipEventRecord")) return -1;
   return check(hipStreamWaitEvent(S(waiter), e, 0), "cn_stream_wait: hipStreamWaitEvent");
@@ -216,6 +240,7 @@ static int mlp_fwd_impl(int codes, const cn_plan* p, const void* d_pack, const f
                         const float* d_xyz, const float* d_viewdir, const float* d_rays_o, const float* d_rays_d,
                         const float* d_z, int z_stride, int n_samples, float* d_sigma, float* d_rgb, void* d_act,
                         int act_M, int act_row0, void* stream) {
+  HotCallScope hot;
   if (codes && !d_act) return fail("cn_mlp_fwd_codes: the activation workspace is required");
   if (!p || !d_pack || !d_blob || !d_sigma || !d_rgb) return fail("cn_mlp_fwd: NULL argument");
   if (check_samples(M, "cn_mlp_fwd")) return -1;
@@ -268,7 +293,7 @@ static int mlp_fwd_impl(int codes, const cn_plan* p, const void* d_pack, const f
     a.pelo = L.pelo ? b + L.pelo + r0 * 64 * es : nullptr;
     for (int i = 0; i < kMaxPlanes; ++i) a.Ylo[i] = L.Ylo[i] ? b + L.Ylo[i] + r0 * L.Yw[i] * es : nullptr;
   }
-  const int grid = (Mp + p->cs.waves_fwd * 32 - 1) / (p->cs.waves_fwd * 32);
+  const int grid = (Mp + p->cs.waves_fwd * p->cs.spw - 1) / (p->cs.waves_fwd * p->cs.spw);
   launch_hot(d_act ? (codes ? p->cs.fwd_codes : p->cs.fwd_train) : p->cs.fwd_infer, dim3(grid),
              dim3(p->cs.waves_fwd * 64), S(stream), a);
   return launch_check("chain_kernel(fwd)");
@@ -293,6 +318,7 @@ int cn_mlp_fwd_codes(const cn_plan* p, const void* d_pack, const float* d_blob, 
 static int mlp_bwd_impl(int codes, const cn_plan* p, const void* d_pack, const float* d_blob, int M,
                         const float* d_dsigma, const float* d_drgb, void* d_act, int act_M, int act_row0,
                         void* stream) {
+  HotCallScope hot;
   if (!p || !d_pack || !d_blob || !d_dsigma || !d_drgb || !d_act) return fail("cn_mlp_bwd: NULL argument");
   if (check_samples(M, "cn_mlp_bwd")) return -1;
   ChainArgs a{};
@@ -321,7 +347,7 @@ static int mlp_bwd_impl(int codes, const cn_plan* p, const void* d_pack, const f
   a.d8 = b + L.d8 + r0 * 32 * es;
   a.spre = (float*)(b + L.spre) + r0;
   a.masks = (uint32_t*)(b + L.masks + (r0 / 32) * L.mask_bytes_per_slab);
-  launch_hot(codes ? p->cs.bwd_codes : p->cs.bwd, dim3((Mp + p->cs.waves_bwd * 32 - 1) / (p->cs.waves_bwd * 32)),
+  launch_hot(codes ? p->cs.bwd_codes : p->cs.bwd, dim3((Mp + p->cs.waves_bwd * p->cs.spw - 1) / (p->cs.waves_bwd * p->cs.spw)),
              dim3(p->cs.waves_bwd * 64), S(stream), a);
   return launch_check("chain_kernel(bwd)");
 }
@@ -344,6 +370,7 @@ int cn_mlp_bwd_codes(const cn_plan* p, const void* d_pack, const float* d_blob, 
 static int mlp_dw_impl(const cn_plan* p, void* d_act, int act_M, int act_row0, int M, const float* d_zvec,
                        const float* const* d_params, float* const* d_grads, float* d_dbuf, int db_accum, int nwg_req,
                        void* d_ws, void* stream) {
+  HotCallScope hot;
   if (!p || !d_act || !d_zvec || !d_params || !d_grads || !d_dbuf || !d_ws) return fail("cn_mlp_dw: NULL argument");
   if (check_samples(M, "cn_mlp_dw")) return -1;
   if (act_M <= 0) act_M = M;
@@ -383,6 +410,7 @@ int cn_mlp_dw_rows(const cn_plan* p, void* d_act, int act_M, int act_row0, int M
 }
 
 int cn_mlp_dbias(const cn_plan* p, void* d_act, int act_M, int M, float* d_dbuf, void* d_ws, void* stream) {
+  HotCallScope hot;
   if (!p || !d_act || !d_dbuf || !d_ws) return fail("cn_mlp_dbias: NULL argument");
   if (check_samples(M, "cn_mlp_dbias")) return -1;
   if (act_M <= 0) act_M = M;

@@ -98,6 +98,12 @@ _OPS_BF16 = dict(fw_w="b", fw_x="b", bw_w="b", bw_dy="b", dw_x="b", dw_dy="b")
 # operands split (the training forward stores their lo parts; encoding_viewdir's
 # dir-PE columns stay hi only), its upstream gradients bf16
 OPS_BF16X3 = dict(fw_w="s", fw_x="s", bw_w="s", bw_dy="s", dw_x="s", dw_dy="b")
+# ... and as the kernels form the latent path's gradient (inj_dy, _lin_inj):
+# from the sum of the bf16 dA plane
+OPS_BF16X3_DB = dict(OPS_BF16X3, inj_dy="b")
+# the built kernels' per-layer exception: encoding_viewdir's dir-PE columns
+# stay hi only in dW (``bf16_operands(ops=..., layer_ops=X3_LAYER_OPS)``)
+X3_LAYER_OPS = {"encoding_viewdir.0": {"dw_x_split_cols": 256}}
 _BF16 = {"on": False, "ops": dict(_OPS_BF16)}
 
 
@@ -181,12 +187,38 @@ def _lin(p, name, x):
     return F.linear(x, p[name + ".weight"], p[name + ".bias"])
 
 
+class _InjSum(torch.autograd.Function):
+    """y + zl with zl (1, F) broadcast over the samples; the backward hands zl
+    the sum over samples of the upstream gradient ROUNDED as ``how`` first --
+    the kernels' latent path: dz = W^T db and dW += db (x) z with db the sum
+    of the stored (bf16) dA plane (dw.hip bias sums), where autograd's
+    broadcast would sum the fp32 gradient."""
+
+    @staticmethod
+    def forward(ctx, y, zl, how):
+        ctx.how = how
+        ctx.zshape = zl.shape
+        return y + zl
+
+    @staticmethod
+    def backward(ctx, dy):
+        d = _q(dy, ctx.how).reshape(-1, dy.shape[-1]).sum(0)
+        return dy, d.reshape(ctx.zshape), None
+
+
 def _lin_inj(p, name, h, z):
     """layer `name` applied to h + z (a latent injection).  In the bf16
     emulation as the kernels compute it: the injection is folded into the
-    layer's bias in fp32 (latent.hip: b + W z), only h is a bf16 operand."""
+    layer's bias in fp32 (latent.hip: b + W z), only h is a bf16 operand; the
+    op ``inj_dy`` ("f" default) rounds the upstream gradient of the latent
+    path before its sum over samples ("b": the kernels' bias sums)."""
     if _BF16["on"]:
-        return _lin(p, name, h) + F.linear(z, p[name + ".weight"])
+        o = _BF16.get("layer_ops", {}).get(name, _BF16["ops"])
+        how = o.get("inj_dy", "f")
+        zl = F.linear(z, p[name + ".weight"])
+        if how == "f":
+            return _lin(p, name, h) + zl
+        return _InjSum.apply(_lin(p, name, h), zl, how)
     return _lin(p, name, h + z)
 
 

@@ -114,6 +114,6 @@ def test_hot_kernels_do_not_spill():
     if not os.path.exists(kr.LIB):
         pytest.skip("library not built")
     ks = kr.kernels()
-    hot = [k for k in ks if "chain_kernel" in k[0] or "dw_kernel" in k[0]]
-    assert len(hot) >= 30, len(hot)
-    assert not [k for k in hot if k[3] > 0], [k for k in hot if k[3] > 0]
+    hot = kr.hot(ks)
+    assert len(hot) >= kr.MIN_HOT, len(hot)
+    assert not [k for k in hot if k[3] > 0 or k[5]], [k for k in hot if k[3] > 0 or k[5]]

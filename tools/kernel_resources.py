@@ -36,7 +36,7 @@ def code_objects(path):
 
 
 def kernels(path=LIB):
-    """[(name, vgpr, agpr, scratch bytes per lane, lds bytes)]"""
+    """[(name, vgpr, agpr, scratch bytes per lane, lds bytes, uses dynamic stack)]"""
     out = []
     for blob in code_objects(path):
         with tempfile.NamedTemporaryFile(suffix=".elf") as f:
@@ -52,20 +52,33 @@ def kernels(path=LIB):
             g = lambda k: int((re.search(rf"^\s*\.{k}:\s+(\d+)", blk, re.M) or [0, -1])[1])
             if g("vgpr_count") < 0:
                 continue
+            dyn = re.search(r"^\s*\.uses_dynamic_stack:\s+(\w+)", blk, re.M)
             out.append((name, g("vgpr_count"), g("agpr_count"), g("private_segment_fixed_size"),
-                        g("group_segment_fixed_size")))
+                        g("group_segment_fixed_size"), bool(dyn and dyn.group(1) in ("true", "1"))))
     return out
 
 
 def spills(path=LIB):
-    return [k for k in kernels(path) if k[3] > 0]
+    """kernels with fixed scratch or a dynamic stack"""
+    return [k for k in kernels(path) if k[3] > 0 or k[5]]
+
+
+def hot(ks):
+    """the hot kernels of a kernel list: chain (forward / dX) and dW"""
+    return [k for k in ks if re.search(r"chain(16)?_kernel|dw_kernel", k[0])]
+
+
+# hot kernels the library must contain: 6 chain sets (fp32 / bf16 / bf16x3 x
+# (3,1) / (2,1)) x 5 chain kernels (fwd train / infer / codes, dX train /
+# codes) + the 2 dW instantiations (bf16 planes, fp32 planes)
+MIN_HOT = 6 * 5 + 2
 
 
 if __name__ == "__main__":
     path = sys.argv[1] if len(sys.argv) > 1 else LIB
     ks = kernels(path)
-    for name, v, a, s, l in ks:
-        print(f"{v:4d} vgpr {a:4d} agpr {s:6d} B scratch {l:7d} B lds  {name}")
-    bad = [k for k in ks if k[3] > 0]
+    for name, v, a, s, l, dyn in ks:
+        print(f"{v:4d} vgpr {a:4d} agpr {s:6d} B scratch {l:7d} B lds {'dyn-stack ' if dyn else ''} {name}")
+    bad = [k for k in ks if k[3] > 0 or k[5]]
     print(f"{len(ks)} kernels, {len(bad)} with scratch")
     sys.exit(1 if bad else 0)

@@ -25,7 +25,7 @@ N_XCD = 8
 
 
 def short(name, prec):
-    m = re.search(r"chain_kernel<(\d), \d, \d, (true|false), \d+, (\d)>", name)
+    m = re.search(r"chain(?:16)?_kernel<(\d), \d, \d, (true|false), \d+, (\d)>", name)
     if m and int(m.group(1)) != prec:
         return None
     if m:

@@ -59,6 +59,15 @@ VARIANTS = {
     "x3_kernel": dict(ops=dict(fw_w=S, fw_x=S, bw_w=S, bw_dy=S, dw_x=S),
                       layer_ops={"encoding_viewdir.0": dict(fw_w=S, fw_x=S, bw_w=S, bw_dy=S, dw_x=S,
                                                             dw_x_split_cols=256)}),
+    # ... with the latent path's gradient from the bf16 dA sums as the kernels
+    # form it (dw.hip bias sums -> dz = W^T db, dW += db (x) z)
+    "x3_kdb": dict(ops=dict(fw_w=S, fw_x=S, bw_w=S, bw_dy=S, dw_x=S, inj_dy=B),
+                   layer_ops={"encoding_viewdir.0": dict(fw_w=S, fw_x=S, bw_w=S, bw_dy=S, dw_x=S,
+                                                         dw_x_split_cols=256)}),
+    # ... and from an exact (split) sum
+    "x3_ksdb": dict(ops=dict(fw_w=S, fw_x=S, bw_w=S, bw_dy=S, dw_x=S, inj_dy=S),
+                    layer_ops={"encoding_viewdir.0": dict(fw_w=S, fw_x=S, bw_w=S, bw_dy=S, dw_x=S,
+                                                          dw_x_split_cols=256)}),
     "x3_kernel_dwall": dict(ops=dict(fw_w=S, fw_x=S, bw_w=S, bw_dy=S, dw_x=S, dw_dy=S),
                             layer_ops={"encoding_viewdir.0": dict(fw_w=S, fw_x=S, bw_w=S, bw_dy=S, dw_x=S,
                                                                   dw_dy=S, dw_x_split_cols=256)}),

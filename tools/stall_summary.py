@@ -19,7 +19,7 @@ def load(d):
     out = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            m = re.search(r"chain_kernel<(\d), \d, \d, (true|false), (\d+), (\d)>", r["Kernel_Name"])
+            m = re.search(r"chain(?:16)?_kernel<(\d), \d, \d, (true|false), (\d+), (\d)>", r["Kernel_Name"])
             d = re.search(r"\bdw_kernel<(\d)>", r["Kernel_Name"])
             if m:
                 k = f"chain<P{m.group(1)},{'bwd' if m.group(2) == 'true' else 'fwd'},{m.group(3)}w,mode{m.group(4)}>"
