@@ -101,6 +101,12 @@ OPS_BF16X3 = dict(fw_w="s", fw_x="s", bw_w="s", bw_dy="s", dw_x="s", dw_dy="b")
 # ... and as the kernels form the latent path's gradient (inj_dy, _lin_inj):
 # from the sum of the bf16 dA plane
 OPS_BF16X3_DB = dict(OPS_BF16X3, inj_dy="b")
+# the kernels' arithmetic op for op (round 5, tools/x3_trace.py): the above,
+# plus ``x3`` -- a product of two split operands is hi*hi + hi*lo + lo*hi
+# (three MFMAs; the lo*lo term dropped) instead of the exact (hi+lo)(hi+lo) --
+# and ``fold`` -- encoding_shape / sigma / encoding_viewdir as the dW pass
+# forms their gradients through the encoding_shape fold (_FoldBlock)
+OPS_BF16X3_K = dict(OPS_BF16X3_DB, x3=True, fold=True)
 # the built kernels' per-layer exception: encoding_viewdir's dir-PE columns
 # stay hi only in dW (``bf16_operands(ops=..., layer_ops=X3_LAYER_OPS)``)
 X3_LAYER_OPS = {"encoding_viewdir.0": {"dw_x_split_cols": 256}}
@@ -132,19 +138,35 @@ def _q(t, how, scale=1.0):
     return hi + _rb(t - hi) if how == "s" else hi
 
 
+def _split(t):
+    hi = _rb(t)
+    return hi, _rb(t - hi)
+
+
+def _mm(a, ha, b, hb, o, gs=1.0):
+    """_q(a, ha) @ _q(b, hb), or -- ``o["x3"]`` and both operands split --
+    the three products the bf16x3 kernels issue (hi hi + hi lo + lo hi: the
+    lo lo term dropped)."""
+    if o.get("x3") and ha == "s" and hb == "s" and gs == 1.0:
+        ah, al = _split(a)
+        bh, bl = _split(b)
+        return ah @ bh + (ah @ bl + al @ bh)
+    return _q(a, ha, gs) @ _q(b, hb)
+
+
 class _Bf16Linear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, o):
         ctx.save_for_backward(x, w)
         ctx.o = o
-        return _q(x, o["fw_x"]) @ _q(w, o["fw_w"]).t() + b
+        return _mm(x, o["fw_x"], w.t(), o["fw_w"], o) + b
 
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
         o = ctx.o
         gs = o.get("grad_scale", 1.0)
-        dx = _q(dy, o["bw_dy"], gs) @ _q(w, o["bw_w"])
+        dx = _mm(dy, o["bw_dy"], w, o["bw_w"], o, gs)
         d2 = _q(dy, o["dw_dy"], gs).reshape(-1, dy.shape[-1])
         n = o.get("dw_x_split_cols")       # the kernels: only the leading n columns split
         if n is None:
@@ -185,6 +207,45 @@ def _lin(p, name, x):
         return _Bf16Linear.apply(x, p[name + ".weight"], p[name + ".bias"],
                                  _BF16.get("layer_ops", {}).get(name, _BF16["ops"]))
     return F.linear(x, p[name + ".weight"], p[name + ".bias"])
+
+
+class _FoldBlock(torch.autograd.Function):
+    """encoding_shape -> (sigma head, encoding_viewdir) as the bf16x3 kernels
+    compute it (``ops["fold"]``; chain_set.h / dw.hip):
+    forward and dX as _Bf16Linear (the sigma head in fp32 from the fp32
+    encoding_shape output); the weight gradients through the encoding_shape
+    fold: Gx = sum_s rn(dA_v) (x) [Y_s | 1] (Y_s split, the sigma row from the
+    split ds), then d[W_v y-part; w_sigma] = Gx [W_e | b_e]^T and
+    d[W_e | b_e] = [W_v; w_sigma]^T Gx in fp32 -- NOT sum rn(dA_e) (x) Y_s,
+    the per-layer restatement's encoding_shape gradient."""
+
+    @staticmethod
+    def forward(ctx, ys, dpe, We, be, Ws, bs, Wv, bv, oe, ov):
+        ye = _mm(ys, oe["fw_x"], We.t(), oe["fw_w"], oe) + be
+        spre = F.linear(ye, Ws, bs)
+        vpre = _mm(torch.cat([ye, dpe], -1), ov["fw_x"], Wv.t(), ov["fw_w"], ov) + bv
+        ctx.save_for_backward(ys, dpe, We, be, Ws, Wv)
+        ctx.o = (oe, ov)
+        return spre, vpre
+
+    @staticmethod
+    def backward(ctx, dspre, dvpre):
+        ys, dpe, We, be, Ws, Wv = ctx.saved_tensors
+        oe, ov = ctx.o
+        F0 = We.shape[0]
+        dye = _mm(dvpre, ov["bw_dy"], Wv[:, :F0], ov["bw_w"], ov) + dspre @ Ws
+        dys = _mm(dye, oe["bw_dy"], We, oe["bw_w"], oe)
+        rA = _q(dvpre, ov["dw_dy"]).reshape(-1, dvpre.shape[-1])
+        ysx = _q(ys, oe["dw_x"]).reshape(-1, ys.shape[-1])
+        dsf = _q(dspre, "s").reshape(-1, 1)
+        Gx, Gb = rA.t() @ ysx, rA.sum(0)
+        Gs, Gsb = dsf.t() @ ysx, dsf.sum(0)
+        dWv = torch.cat([Gx @ We.t() + Gb[:, None] * be[None, :],
+                         rA.t() @ _q(dpe, "b").reshape(-1, dpe.shape[-1])], 1)
+        dWs = Gs @ We.t() + Gsb[:, None] * be[None, :]
+        dWe = Wv[:, :F0].t() @ Gx + Ws.t() @ Gs
+        dbe = Wv[:, :F0].t() @ Gb + Ws[0] * Gsb
+        return dys, None, dWe, dbe, dWs, Gsb, dWv, Gb, None, None
 
 
 class _InjSum(torch.autograd.Function):
@@ -239,12 +300,22 @@ def codenerf_forward(p, xyz, viewdir, shape_code, texture_code, shape_blocks=3,
         h = F.relu(_lin_inj(p, f"shape_layer_{j}.0", h, z))
         if acts is not None:
             acts[f"y{j}"] = h
-    h = _lin(p, "encoding_shape", h)
-    if acts is not None:
-        acts["y_shape"] = h
-    sig = F.softplus(_lin(p, "sigma.0", h), beta=1.0, threshold=20.0)
-    h = F.relu(_lin(p, "encoding_viewdir.0",
-                    torch.cat([h, positional_encoding(viewdir, num_dir_freq)], -1)))
+    if _BF16["on"] and _BF16["ops"].get("fold") and acts is None:
+        lo = _BF16.get("layer_ops", {})
+        dpe = positional_encoding(viewdir, num_dir_freq)
+        spre, vpre = _FoldBlock.apply(h, dpe, p["encoding_shape.weight"], p["encoding_shape.bias"],
+                                      p["sigma.0.weight"], p["sigma.0.bias"], p["encoding_viewdir.0.weight"],
+                                      p["encoding_viewdir.0.bias"], lo.get("encoding_shape", _BF16["ops"]),
+                                      lo.get("encoding_viewdir.0", _BF16["ops"]))
+        sig = F.softplus(spre, beta=1.0, threshold=20.0)
+        h = F.relu(vpre)
+    else:
+        h = _lin(p, "encoding_shape", h)
+        if acts is not None:
+            acts["y_shape"] = h
+        sig = F.softplus(_lin(p, "sigma.0", h), beta=1.0, threshold=20.0)
+        h = F.relu(_lin(p, "encoding_viewdir.0",
+                        torch.cat([h, positional_encoding(viewdir, num_dir_freq)], -1)))
     if acts is not None:
         acts["y_view"] = h
     for j in range(1, texture_blocks + 1):

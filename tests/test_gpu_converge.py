@@ -32,7 +32,7 @@ meaningful, and convergence separately:
    not asserted.  bf16x3 against the fp32 replay: leaves 0.05 dB at step 19
    (0.09 dB; round 4) where the reference computed on the GPU stays within
    0.025 dB of the CPU one for 29 steps: asserted over the first 18 steps,
-   and against the replay of its OWN arithmetic (ref_cpu.OPS_BF16X3_DB) over
+   and against the replay of its OWN arithmetic (ref_cpu.OPS_BF16X3_K) over
    its replayable prefix (>= 15 steps).
 2. CONVERGENCE over ITERS steps for several initialisations: fp32 and bf16
    both exceed 20 dB (best 50-step mean).  The bf16 - fp32 gap of the final
@@ -100,15 +100,15 @@ def _run(tmp_path, root, name, prec, overlap, init_seed, iters, init=None):
 def _replay(root, init, seed, steps, bf16, x3=False):
     """The CPU replay of the reference loop: fp32, or at the bf16 kernels'
     operand precision (bf16), or at the bf16x3 kernels' (x3: hi + lo
-    operands, the dW X split, the latent path from the bf16 dA sums --
-    ref_cpu.OPS_BF16X3_DB / X3_LAYER_OPS)."""
+    operands in three products, the dW X split, the latent path from the bf16
+    dA sums, the encoding_shape fold -- ref_cpu.OPS_BF16X3_K / X3_LAYER_OPS)."""
     from oracle import ref_cpu
     from test_gpu_train import _oracle_training
     torch.set_num_threads(min(16, os.cpu_count() or 1))
     torch.manual_seed(1000 + seed)
     np.random.seed(1000 + seed)
     if x3:
-        with ref_cpu.bf16_operands(ops=ref_cpu.OPS_BF16X3_DB, layer_ops=ref_cpu.X3_LAYER_OPS):
+        with ref_cpu.bf16_operands(ops=ref_cpu.OPS_BF16X3_K, layer_ops=ref_cpu.X3_LAYER_OPS):
             ps, _, _, _ = _oracle_training(_hp(root, "fp32"), init, steps, 256)
     elif bf16:
         with ref_cpu.bf16_operands():
@@ -151,7 +151,7 @@ def test_early_train_psnr_matches_reference_at_each_precision(tmp_path):
     # instead of the CPU).  bf16x3 is held to (a) the north-star 0.05 dB of
     # the fp32 replay over the first X3_FP32_STEPS steps (measured round 4:
     # it first leaves at step 19) and (b) 0.05 dB of the replay of ITS OWN
-    # arithmetic (ref_cpu.OPS_BF16X3_DB) over bf16x3's replayable prefix,
+    # arithmetic (ref_cpu.OPS_BF16X3_K) over bf16x3's replayable prefix,
     # >= X3_PREFIX steps -- the kernels compute what their emulation computes
     # (as the bf16 case above).
     from test_gpu_regime import chaos_horizon, first_exit

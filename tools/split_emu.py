@@ -110,6 +110,9 @@ for _l in _LAYERS:
 def main():
     from codenerf_amd.data import make_synthetic_srn
     from oracle import ref_cpu
+    # the kernels' arithmetic op for op (round 5): + the three-MFMA products
+    # (lo lo dropped) and the encoding_shape fold (ref_cpu.OPS_BF16X3_K)
+    VARIANTS["x3_k"] = dict(ops=ref_cpu.OPS_BF16X3_K, layer_ops=ref_cpu.X3_LAYER_OPS)
     from oracle.params import make_params, make_codes
     from test_gpu_train import _oracle_training
     regime = sys.argv[1] if len(sys.argv) > 1 else "one"

@@ -120,7 +120,7 @@ def main():
         res = {}
         res["x3"], lx3 = hip_step("bf16x3", *args)
         res["f32"], _ = hip_step("fp32", *args)
-        emu = dict(ops=ref_cpu.OPS_BF16X3_DB, layer_ops=ref_cpu.X3_LAYER_OPS)
+        emu = dict(ops=ref_cpu.OPS_BF16X3_K, layer_ops=ref_cpu.X3_LAYER_OPS)
         res["emuG"], _ = oracle_step(*args, device="cuda", **emu)
         res["emuC"], _ = oracle_step(*args, **emu)
         res["t32"], _ = oracle_step(*args)
