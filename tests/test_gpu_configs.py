@@ -461,8 +461,12 @@ def test_module_forward_over_budget_recomputes_parts(monkeypatch):
     recomputes each part in the backward: outputs bit-identical to the
     one-workspace path, and the gradients of BOTH paths as accurate as the
     reference's own fp32 arithmetic, measured against a float64 replay of the
-    oracle (per tensor: rel-L2 err(ours) <= 2 err(torch fp32 oracle) + 1e-6;
-    the two paths group the fp32 sums over 65 K samples differently)."""
+    oracle (per tensor: rel-L2 err(ours) <= 2 err(torch fp32 oracle) + the
+    rounding of one M-term fp32 sum in sequential order, sqrt(M) 2^-24 =
+    1.5e-5 at M = 65,536 samples: torch's pairwise sums can be far better than
+    that on a cancelling bias sum -- measured round 5: rgb.0.bias 9.9e-6 /
+    3.5e-6 for the two paths against torch's 1.6e-7; test_gpu_parity.py's
+    floor is 2e-4)."""
     from codenerf_amd import engine as _eng
     dev = _dev()
     params = make_params(51)
@@ -498,6 +502,6 @@ def test_module_forward_over_budget_recomputes_parts(monkeypatch):
         e_ref = _rel_l2(r32, r64)
         for j, o in enumerate(out):
             e = _rel_l2(o[2][i], r64)
-            if e > 2 * e_ref + 1e-6:
+            if e > 2 * e_ref + np.sqrt(B * N) * 2.0 ** -24:
                 bad.append((i, j, e, e_ref))
     assert not bad, bad

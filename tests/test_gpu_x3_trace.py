@@ -1,0 +1,68 @@
+"""GPU: does the HIP bf16x3 step compute what its emulation computes, tensor
+by tensor?  (round-4 verdict item 1; tools/x3_trace.py is the full record.)
+
+At the state where seed 3 of test_gpu_regime.py's many-object regime
+separates (step 104: epoch 13 of the HIP fp32 trajectory), one training image
+goes through the HIP bf16x3 step and through the loop's restatement under the
+kernels' arithmetic (oracle/ref_cpu.py OPS_BF16X3_K: hi + lo operands in three
+products, the dW X split with encoding_viewdir's dir-PE tile hi only, the
+latent path from the bf16 dA sums, the encoding_shape fold) in torch on the
+GPU (emuG) and on the CPU (emuC, a second fp32 summation order).  Per
+parameter / code tensor the kernel's distance to emuG must be of the size of
+emuG's distance to emuC: the kernel differs from its emulation by
+fp32-order noise, amplified through the bf16 roundings both apply.
+Measured round 5 (profiles/r05f/trace_seed3_k.log): ratios 0.9-1.2 on 27 of
+30 tensors, 2.6-3.7 on encoding_shape and encoding_viewdir; the emulation
+without the fold (OPS_BF16X3_DB) was 17-41x off on encoding_shape
+(profiles/r05d/trace_seed3.log).
+"""
+import os
+import pathlib
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+RATIO = 5.0
+
+
+@pytest.mark.timeout(600)
+def test_bf16x3_kernels_match_their_emulation_per_tensor(tmp_path):
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import x3_trace
+    import test_gpu_regime as R
+    from codenerf_amd.data import SRN, collate_one
+    from oracle import ref_cpu
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    seed, k = 3, 104
+    root = R._data(tmp_path)
+    hp = R.hp_many(root, "fp32")
+    R._run(tmp_path, root, "fp32", k, seed=seed)
+    tr = R._run.last
+    sd = {n: v.detach().cpu().clone() for n, v in tr.model.state_dict().items()}
+    shape = tr.shape_codes.weight.detach().cpu().clone()
+    tex = tr.texture_codes.weight.detach().cpu().clone()
+    oi = k % R.N_OBJ
+    ds = SRN("srn_cars", "cars_train", root, 1, crop_img=False, n_train_views=2)
+    np.random.seed(5000 + k)
+    focal, H, W, imgs, poses, _, _ = collate_one(ds[oi])
+    ro, vd = ref_cpu.get_rays(int(H), int(W), focal, poses[0, 0])
+    g = torch.Generator().manual_seed(7000 + k)
+    z = ref_cpu.stratified_z(hp["near"], hp["far"], hp["N_samples"], jitter=torch.rand(hp["N_samples"], generator=g))
+    args = (sd, shape, tex, oi, ro, vd, z, imgs[0, 0].contiguous(), R.B)
+    x3, _ = x3_trace.hip_step("bf16x3", *args)
+    emu = dict(ops=ref_cpu.OPS_BF16X3_K, layer_ops=ref_cpu.X3_LAYER_OPS)
+    emug, _ = x3_trace.oracle_step(*args, device="cuda", **emu)
+    emuc, _ = x3_trace.oracle_step(*args, **emu)
+    bad = []
+    for name in emug:
+        d_k = x3_trace._rel(x3[name], emug[name])
+        d_n = x3_trace._rel(emug[name], emuc[name])
+        print(f"{name:32s} x3~emuG {d_k:.2e}  emuG~emuC {d_n:.2e}  ratio {d_k / d_n:5.2f}")
+        if d_k > RATIO * d_n + 1e-7:
+            bad.append((name, d_k, d_n))
+    assert not bad, bad
