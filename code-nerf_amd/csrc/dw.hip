@@ -59,28 +59,35 @@ template <> struct DwShape<DW_RGB2>    { static constexpr int kA = 1, kX0 = 4, k
 // 256x256 bodies measured 0.2 ms slower per C2 step.
 constexpr int kDwSmem = 160 * 1024;
 
-// Hi-only bodies (bf16 planes, fp32 planes); the bf16x3 planes' LO bodies
-// are DwLo below.
-template <int P, int KIND>
+// LO (bf16x3 planes): the slab also stages X0's lo parts (after X1), and every
+// X0 fragment's MFMA is followed by one with the lo fragment, so dW sums
+// A (x) (X0_hi + X0_lo) -- the X operand at ~16 significant bits, as the
+// bf16x3 chains used it.  The dir-PE tile (X1) stays hi only.
+template <int P, int KIND, bool LO = false>
 struct DwBody {
   using Sh = DwShape<KIND>;
   static constexpr bool kBf16 = P == CN_P_BF16;
+  static_assert(kBf16 || !LO, "lo planes exist for bf16 planes only");
   static constexpr int ES = kBf16 ? 2 : 4;
   static constexpr int TB = 1024 * ES;                      // one 32-sample x 32-feature tile
   static constexpr int kA = Sh::kA, kX0 = Sh::kX0, kX1 = Sh::kX1, NI = Sh::NI, NJ = Sh::NJ;
+  static constexpr int kXl = LO ? kX0 : 0;                  // lo tiles of X0
   static constexpr int kPA = kA * TB / 1024, kPX0 = kX0 * TB / 1024;   // 1 KiB pieces of A / X0
   static constexpr int kPX1 = kX1 * TB / 1024;
-  static constexpr int kPieces = (kA + kX0 + kX1) * TB / 1024;     // 1 KiB pieces per slab
+  static constexpr int kPieces = (kA + kX0 + kX1 + kXl) * TB / 1024;     // 1 KiB pieces per slab
   static constexpr int kG = (kPieces + 7) / 8;              // pieces per wave per slab
   static constexpr bool kVD = KIND == DW_VIEWDIR;
-  // bf16: 32 / 36 KiB slots, 4-slot ring (measured best)
-  static constexpr int kDwSlot = kBf16 ? (KIND == DW_FULL ? 32 * 1024 : 36 * 1024) : 72 * 1024;
+  // hi-only bf16: 32 / 36 KiB slots, 4-slot ring (measured best); LO: the
+  // slab itself, as many slots (<= 4) as fit beside the padding pieces
+  static constexpr int kLoRing = (kDwSmem - (8 * kG - kPieces) * 1024) / (kPieces * 1024);
+  static constexpr int kDwSlot = LO ? kPieces * 1024 : kBf16 ? (KIND == DW_FULL ? 32 * 1024 : 36 * 1024) : 72 * 1024;
   // Paired staging (the bf16 256 x 256 bodies): one barrier and one 64 KiB
   // DMA batch per TWO slabs over a 5-slot ring (three slabs in flight while
-  // two are consumed) -- 48 KiB batches streamed at 6.2 TB/s where per-slab
-  // 32 KiB batches stream at 5.5 (profiles/r04c, r04e)
-  static constexpr bool kPair = kBf16 && KIND == DW_FULL;
-  static constexpr int kDwRing = kPair ? 5 : kBf16 ? 4 : 2;
+  // two are consumed) -- the LO bodies' 48 KiB batches streamed at 6.2 TB/s
+  // where per-slab 32 KiB batches stream at 5.5 (profiles/r04c, r04e)
+  static constexpr bool kPair = kBf16 && !LO && KIND == DW_FULL;
+  static constexpr int kDwRing = kPair ? 5 : LO ? (kLoRing < 4 ? kLoRing : 4) : kBf16 ? 4 : 2;
+  static_assert(!LO || kDwRing >= 3, "a LO slab must leave a 3-slot ring");
   static constexpr int kDwDepth = kPair ? 3 : kDwRing - 1;   // slabs issued before the first barrier
   static constexpr int kDwDummy = kDwRing * kDwSlot;  // landing area of padding pieces
   static_assert(kPieces * 1024 <= kDwSlot, "dw stage");
@@ -132,6 +139,7 @@ struct DwBody {
     const char* pa = (const char*)pr.A;
     const char* px0 = (const char*)pr.X0;
     const char* px1 = kX1 ? (const char*)pr.X1 : px0;
+    const char* px0l = LO ? (const char*)pr.X0lo : px0;
     auto issue = [&](int st, auto slotc) {
       const size_t t = (size_t)slab(st);
 #pragma unroll
@@ -142,6 +150,7 @@ struct DwBody {
         if (piece < kPA) src = pa + t * (kA * TB) + piece * 1024;
         else if (piece < kPA + kPX0) src = px0 + t * (kX0 * TB) + (piece - kPA) * 1024;
         else if (piece < kPA + kPX0 + kPX1) src = px1 + t * (kX1 * TB) + (piece - kPA - kPX0) * 1024;
+        else if (piece < kPieces) src = px0l + t * (kX0 * TB) + (piece - kPA - kPX0 - kPX1) * 1024;
         else {
           src = pa + t * (kA * TB);              // padding piece: re-read, never consumed
           dst = lds_addr(smem + kDwDummy + (piece - kPieces) * 1024);
@@ -192,6 +201,7 @@ struct DwBody {
       }
       const char* A = smem + SL * kDwSlot;
       const char* X = A + kA * TB;
+      const char* Xl = X + (kX0 + kX1) * TB;     // LO: X0's lo tiles
       if (!live) return;
       if constexpr (!kBf16) {
         // exact fp32: K = 2 samples per MFMA; lane l reads feature l & 31 of
@@ -248,6 +258,8 @@ struct DwBody {
         bf16x8 fs{};
         if constexpr (kVD) fs = frag(A, 8, s);   // sigma-head columns 256.. of the dA plane
         bf16x8 fx = frag(X, col_tile(w, 0), s);
+        bf16x8 fxl{};
+        if constexpr (LO) fxl = frag(Xl, col_tile(w, 0), s);
         // bias sums (VALU) while the reads are in flight
 #pragma unroll
         for (int i = 0; i < NI; ++i)
@@ -257,15 +269,28 @@ struct DwBody {
         }
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-          bf16x8 nx{};
+          bf16x8 nx{}, nxl{};
           if (j + 1 < NJ) {
             nx = frag(X, col_tile(w, j + 1), s);
+            if constexpr (LO) nxl = frag(Xl, col_tile(w, j + 1), s);
           } else if constexpr (kVD) {
             nx = frag(X, 8, s);                  // the dir-PE input tile, for acc_e1 below
           }
 #pragma unroll
           for (int i = 0; i < NI; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fx, acc[i][j], 0, 0, 0);
+          if constexpr (kVD && LO) {      // (LO: no registers left for a re-read after the loop)
+            if (j == (w >> 1)) acc_e2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fs, fx, acc_e2, 0, 0, 0);
+          }
+          if constexpr (LO) {
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fxl, acc[i][j], 0, 0, 0);
+            if constexpr (kVD) {
+              if (j == (w >> 1)) acc_e2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fs, fxl, acc_e2, 0, 0, 0);
+            }
+          }
           fx = nx;
+          fxl = nxl;
         }
         if constexpr (kVD) {
           const bf16x8 fr = (w & 1) ? fa[1] : fa[0];
@@ -273,7 +298,8 @@ struct DwBody {
           // the sigma-head tile against this wave's column tile w >> 1 of its
           // half, read once more instead of a wave-uniform branch inside the
           // unrolled column loop (each branch target cost hazard NOPs)
-          acc_e2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fs, frag(X, 4 * (w & 1) + (w >> 1), s), acc_e2, 0, 0, 0);
+          if constexpr (!LO)
+            acc_e2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fs, frag(X, 4 * (w & 1) + (w >> 1), s), acc_e2, 0, 0, 0);
         }
       }
     };
@@ -282,13 +308,8 @@ struct DwBody {
         if (base + k < nst) body(base + k, k);
       });
     __syncthreads();
-    write_partials(acc, acc_e1, acc_e2, dbacc, dbsig, live, do_db, lane, w, h, part, dbpart);
-  }
 
-  // ---- fp32 partial: row n (out feature), column c (in feature)
-  __device__ static void write_partials(const f32x16 (&acc)[NI][NJ], const f32x16& acc_e1, const f32x16& acc_e2,
-                                        const float* dbacc, float dbsig, bool live, bool do_db, int lane, int w,
-                                        int h, float* part, float* dbpart) {
+    // ---- fp32 partial: row n (out feature), column c (in feature)
     if (live) {
 #pragma unroll
       for (int i = 0; i < NI; ++i)
@@ -325,144 +346,6 @@ struct DwBody {
   }
 };
 
-template <int KIND>
-struct DwLo {
-  using Sh = DwShape<KIND>;
-  static constexpr int kA = Sh::kA, kX0 = Sh::kX0, kX1 = Sh::kX1, NI = Sh::NI, NJ = Sh::NJ;
-  static constexpr int kT = kA + 2 * kX0 + kX1;             // tiles per slab
-  static constexpr int kRing = kDwSmem / 2048;              // tile slots
-  static constexpr int kSteady = (2 * (kRing - 2 * kT)) / 8;   // vmcnt at a steady-state barrier
-  static_assert(2 * kT <= kRing, "two LO slabs must fit the ring");
-  static constexpr bool kVD = KIND == DW_VIEWDIR;
-  using B = DwBody<CN_P_BF16, KIND>;
-
-  __device__ static void run(const DwProblem& pr, int t0, int t1, int rot, float* part, float* dbpart, char* smem) {
-    const int nst = t1 - t0;
-    rot %= nst;
-    auto slab = [&](int st) { const int t = st + rot; return t0 + (t >= nst ? t - nst : t); };
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int h = lane >> 5;
-    const bool live = B::wave_live(w);
-    const bool do_db = B::wave_db(w);
-
-    f32x16 acc[NI][NJ];
-#pragma unroll
-    for (int i = 0; i < NI; ++i)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x16{};
-    f32x16 acc_e1 = f32x16{}, acc_e2 = f32x16{};     // viewdir: (row w, dir tile), (sigma tile, col)
-    float dbacc[NI];
-#pragma unroll
-    for (int i = 0; i < NI; ++i) dbacc[i] = 0.f;
-    float dbsig = 0.f;
-
-    const char* pa = (const char*)pr.A;
-    const char* px0 = (const char*)pr.X0;
-    const char* px1 = kX1 ? (const char*)pr.X1 : px0;
-    const char* px0l = (const char*)pr.X0lo;
-    const uint32_t ring = lds_addr(smem);
-    const int total = 2 * kT * nst;                 // DMA instructions of this segment
-    // issue this wave's instructions of [i0, i1) (wave-uniform bounds)
-    auto issue = [&](int i0, int i1) {
-      i1 = min(i1, total);
-      for (int I = i0 + ((w - i0) & 7); I < i1; I += 8) {
-        const int p = I >> 1, s = p / kT, k = p - s * kT;
-        const size_t t = (size_t)slab(s);
-        const char* src;
-        if (k < kA) src = pa + (t * kA + k) * 2048;
-        else if (k < kA + kX0) src = px0 + (t * kX0 + (k - kA)) * 2048;
-        else if (k < kA + kX0 + kX1) src = px1 + (t * kX1 + (k - kA - kX0)) * 2048;
-        else src = px0l + (t * kX0 + (k - kA - kX0 - kX1)) * 2048;
-        glds16_opaque_nt(src + (I & 1) * 1024 + lane * 16, ring + (p % kRing) * 2048 + (I & 1) * 1024);
-      }
-    };
-    issue(0, 2 * kRing);
-
-    const int G = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-    // in-tile byte offset of this lane's transposed read (features 16 (G & 1) + 4 p)
-    const int f = 16 * (G & 1) + 4 * p;
-    auto frag = [&](uint32_t tbase, int s) -> bf16x8 {
-      s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(tbase + img_off<2>(s, f)));
-      s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(tbase + img_off<2>(s + 4, f)));
-      return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-    };
-    auto rowsum = [](bf16x8 v) {
-      float sum = 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) sum += (float)v[j];
-      return sum;
-    };
-
-    int base = 0;      // slot of the current slab's tile 0 (kT st % kRing)
-    for (int st = 0; st < nst; ++st) {
-      // this slab landed: at most the wave's instructions of the window
-      // [2 kT (st + 1), issued) may still be in flight
-      const int issued = min(total, 2 * (st == 0 ? kRing : kT * (st - 1) + kRing));
-      const int n = max(0, min(kSteady, (issued - 2 * kT * (st + 1)) >> 3));
-      static_for<0, kSteady + 1>([&](auto c) {
-        if (n == c) wait_vmcnt<c>();
-      });
-      block_barrier();
-      // every wave is past slab st - 1: its slots take tiles up to kT st + kRing
-      if (st > 0) issue(2 * (kT * (st - 1) + kRing), 2 * (kT * st + kRing));
-      auto tb = [&](int k) {             // LDS address of this slab's tile k
-        const int sl = base + k;
-        return ring + (uint32_t)((sl >= kRing ? sl - kRing : sl) * 2048);
-      };
-      base += kT;
-      if (base >= kRing) base -= kRing;
-      if (!live) continue;
-#pragma unroll
-      for (int kk = 0; kk < 32; kk += 16) {
-        const int s = kk + 8 * h + q;
-        bf16x8 fa[NI];
-#pragma unroll
-        for (int i = 0; i < NI; ++i) fa[i] = frag(tb(B::row_tile(w, i)), s);
-        bf16x8 fs{};
-        if constexpr (kVD) fs = frag(tb(8), s);   // sigma-head columns 256.. of the dA plane
-        bf16x8 fx = frag(tb(kA + B::col_tile(w, 0)), s);
-        bf16x8 fxl = frag(tb(kA + kX0 + kX1 + B::col_tile(w, 0)), s);
-#pragma unroll
-        for (int i = 0; i < NI; ++i)
-          if (do_db) dbacc[i] += rowsum(fa[i]);
-        if constexpr (kVD) {
-          if (w == 0) dbsig += rowsum(fs);
-        }
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          bf16x8 nx{}, nxl{};
-          if (j + 1 < NJ) {
-            nx = frag(tb(kA + B::col_tile(w, j + 1)), s);
-            nxl = frag(tb(kA + kX0 + kX1 + B::col_tile(w, j + 1)), s);
-          } else if constexpr (kVD) {
-            nx = frag(tb(kA + kX0), s);          // the dir-PE input tile, for acc_e1 below
-          }
-#pragma unroll
-          for (int i = 0; i < NI; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fx, acc[i][j], 0, 0, 0);
-          if constexpr (kVD) {
-            if (j == (w >> 1)) acc_e2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fs, fx, acc_e2, 0, 0, 0);
-          }
-#pragma unroll
-          for (int i = 0; i < NI; ++i)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fxl, acc[i][j], 0, 0, 0);
-          if constexpr (kVD) {
-            if (j == (w >> 1)) acc_e2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fs, fxl, acc_e2, 0, 0, 0);
-          }
-          fx = nx;
-          fxl = nxl;
-        }
-        if constexpr (kVD) {
-          const bf16x8 fr = (w & 1) ? fa[1] : fa[0];
-          acc_e1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr, fx, acc_e1, 0, 0, 0);   // fx = the dir-PE tile
-        }
-      }
-    }
-    __syncthreads();
-    B::write_partials(acc, acc_e1, acc_e2, dbacc, dbsig, live, do_db, lane, w, h, part, dbpart);
-  }
-};
-
 template <int P>
 __global__ __launch_bounds__(512, 2) void dw_kernel(DwArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[kDwSmem];
@@ -478,12 +361,12 @@ __global__ __launch_bounds__(512, 2) void dw_kernel(DwArgs a) {
     const DwProblem& pr = a.p[p];
     float* part = a.part + slot * kPartRows * kPartCols;
     float* dbpart = a.dbpart + slot * kPartRows;
-    // bf16x3 planes: the X0 lo parts ride along (pr.lo, DwLo)
+    // bf16x3 planes: the X0 lo parts ride along (pr.lo, DwBody<..., true>)
     auto body = [&](auto kind) {
       constexpr int K = decltype(kind)::value;
       if constexpr (P == CN_P_BF16) {
         if (pr.lo) {
-          DwLo<K>::run(pr, t0, t1, g * 613, part, dbpart, smem);
+          DwBody<P, K, true>::run(pr, t0, t1, g * 613, part, dbpart, smem);
           return;
         }
       }
