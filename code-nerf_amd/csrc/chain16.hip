@@ -78,13 +78,21 @@ struct Chain16 {
   static constexpr int NL = S::NL;
   static constexpr int kChunks = S::kChunks;
   static constexpr int kSpw = 16;                          // samples per wave
-  static_assert(kChunkBlocks % WAVES == 0, "every wave issues an equal share of a chunk");
-  static constexpr int G = kChunkBlocks / WAVES;           // LDS-DMA instructions per wave per chunk
+  // waves that issue the weight stream's LDS-DMA: all of them when WAVES
+  // divides a chunk; of a 12-wave workgroup, waves 0-7 (2 blocks each)
+  static constexpr int kIssuers = kChunkBlocks % WAVES == 0 ? WAVES : 8;
+  static_assert(kChunkBlocks % kIssuers == 0, "issuing waves must divide a chunk");
+  static constexpr int G = kChunkBlocks / kIssuers;        // LDS-DMA instructions per issuing wave per chunk
   // chunks in flight: a 16 KiB chunk feeds one wave 8 (bf16x3: 24) MFMAs of
-  // 16 cycles, two waves per SIMD; ~1.1 us from LDS-DMA issue to landing
-  static constexpr int D = kX3 ? 5 : 4;
+  // 16 cycles, two or three waves per SIMD; ~1.1 us from LDS-DMA issue to
+  // landing (a 12-wave backward keeps 4: its mask words take the LDS)
+  static constexpr int D = (kX3 && !(BWD && WAVES > 8)) ? 5 : 4;
   static constexpr int NS = D + 2;                         // ring slots (see chain.hip)
-  static constexpr int kPF = 3;                            // A-fragment prefetch distance (blocks)
+  // A-fragment prefetch distance (blocks): 12-wave workgroups (three waves
+  // per SIMD hide the LDS latency) read the forward's fragments in place and
+  // the backward's one block ahead, which keeps them within the 168
+  // registers of three waves
+  static constexpr int kPF = WAVES > 8 ? (BWD ? 1 : 0) : 3;
   static constexpr int kSbMask = 0x6;
   static constexpr int kRingBytes = NS * kChunkBytes;
   static constexpr int kBlobFloats = BiasBlob<SB, TB>::kFloats;
@@ -105,46 +113,104 @@ struct Chain16 {
     const int p = S::L(i).plane;
     return BWD ? ((PLANES && N::stored(p)) || codes_plane(p)) : (PLANES && p >= 0 && N::stored(p));
   }
-  // ---------------- epilogue schedule ("diagonal", as chain.hip): tile t of
-  // layer i feeds k-block t / 2 of layer i + 1.  Tiles 0-3 are converted at
-  // the layer's last block, tile t >= 4 after k-block t / 2 - 2 of the next
-  // layer's first tile (one k-block before the one that reads it), so the
-  // conversion VALU issues between MFMAs instead of as one burst.
-  static constexpr bool diag(int i) { return i + 1 < NL && S::L(i).epi != EPI_RGB; }
+  // ---------------- epilogue schedule: the tile pipeline (round 5).  Tile t
+  // of layer i is converted (ReLU, mask bits, hi / lo split, plane stores)
+  // after the SECOND block of tile t + 1 of the same layer -- the last tile
+  // after the second block of the next layer's first tile -- so its VALU
+  // issues among tile t + 1's MFMAs, evenly over the layer, instead of as
+  // bursts at layer boundaries (a 16x16x32 MFMA leaves the vector issue free
+  // for only 8 of its 16 cycles: the round-5 counters put the chains at
+  // MFMA busy 0.65 with 0.02 MFMA / VALU co-execution when every tile of a
+  // layer was converted inside the next layer's first tile).  A layer reads
+  // its input k-blocks from one operand array and writes its output tiles
+  // into the other (X[i & 1] -> X[(i & 1) ^ 1]); two accumulator tiles are
+  // live (acc[t & 1]).
+  static constexpr bool converts(int i) { return S::L(i).epi != EPI_RGB; }
+  static constexpr int tile_first(int i, int t) { return S::first_block(i) + t * S::bpt(i); }
+  // (the backward's last layer, with no next layer: its last tile at its own
+  // last block)
   static constexpr int conv_block(int i, int t) {
-    return (!diag(i) || t < 4) ? S::last_block(i) : S::first_block(i + 1) + S::kAmul * ((t >> 1) - 1) - 1;
+    return t + 1 < S::tiles(i) ? tile_first(i, t + 1) + (S::bpt(i) > 1 ? 1 : 0)
+           : i + 1 < NL        ? S::first_block(i + 1) + (S::bpt(i + 1) > 1 ? 1 : 0)
+                               : S::last_block(i);
   }
   static constexpr int final_block(int i) { return conv_block(i, S::tiles(i) - 1); }
-  static constexpr int conv_layer_at(int g) {
-    for (int i = 0; i < NL; ++i)
-      if (S::L(i).epi != EPI_RGB && g >= S::last_block(i) && g <= final_block(i))
-        for (int t = 0; t < S::tiles(i); ++t)
-          if (conv_block(i, t) == g) return i;
+  static constexpr bool sched_ok() {
+    for (int i = 0; i < NL; ++i) {
+      if (!converts(i)) continue;
+      const int T = S::tiles(i);
+      if (T % 2) return false;                            // acc[t & 1] hand-over to the next layer
+      // the last tile is converted before the next layer reads its k-block
+      if (i + 1 < NL && final_block(i) >= S::first_block(i + 1) + ((T - 1) >> 1) * S::kAmul) return false;
+      // and before tile t + 2 reuses its accumulator
+      for (int t = 0; t < T; ++t) {
+        if (t + 2 < T && conv_block(i, t) >= tile_first(i, t + 2)) return false;
+        if (conv_at(conv_block(i, t)) != 64 * i + t) return false;      // conv_at inverts conv_block
+      }
+    }
+    return true;
+  }
+  // (layer, tile) converted after block g: 64 layer + tile, or -1 (the
+  // inverse of conv_block, cheap enough for the vmcnt bookkeeping's
+  // compile-time loops)
+  static constexpr int conv_at(int g) {
+    const int li = S::layer_of(g), lb = g - S::first_block(li);
+    const int tn = lb / S::bpt(li), r = lb % S::bpt(li), r1 = S::bpt(li) > 1 ? 1 : 0;
+    if (r == r1 && tn >= 1 && converts(li)) return 64 * li + tn - 1;
+    if (r == r1 && tn == 0 && li >= 1 && converts(li - 1)) return 64 * (li - 1) + S::tiles(li - 1) - 1;
+    if (li == NL - 1 && g == S::last_block(li) && converts(li)) return 64 * li + S::tiles(li) - 1;
     return -1;
   }
-  static constexpr int conv_first_tile(int i, int g) {
-    for (int t = 0; t < S::tiles(i); ++t)
-      if (conv_block(i, t) == g) return t;
-    return 0;
+  static_assert(sched_ok(), "tile pipeline schedule");
+
+  // ---------------- LDS read groups.  Every LDS read inside the block loop is
+  // an explicit ds_read whose lgkmcnt wait is counted at compile time, so the
+  // compiler (which would wait lgkmcnt(0) behind a read it can see, draining
+  // every fragment prefetch in flight) emits none.  Group x -- issued kPF
+  // blocks before block x -- reads, in order: block x's A fragment; the bias
+  // tile when x starts a forward output tile (the MFMA's C operand); the
+  // sigma-head weights when the tile converted after block x needs them
+  // (encoding_shape forward, encoding_viewdir backward); the mask word when a
+  // backward tile converted after block x is masked.
+  static constexpr int tile_of(int g) { return (g - S::first_block(S::layer_of(g))) / S::bpt(S::layer_of(g)); }
+  static constexpr bool has_bias(int x) {
+    return !BWD && (x - S::first_block(S::layer_of(x))) % S::bpt(S::layer_of(x)) == 0;
   }
-  static constexpr int conv_tiles(int i, int g) {
+  static constexpr bool has_ws(int x) {
+    const int c = conv_at(x);
+    return c >= 0 && S::L(c / 64).epi == (BWD ? EPI_BSIGMA : EPI_SHAPE);
+  }
+  static constexpr bool has_mask(int x) { const int c = conv_at(x); return BWD && c >= 0 && S::L(c / 64).epi == EPI_BMASK; }
+  static constexpr int group_reads(int x) {
+    return x < 0 || x >= S::kBlocks ? 0 : 1 + has_bias(x) + has_ws(x) + has_mask(x);
+  }
+  // reads issued after group g's last one, up to group g + kPF (issued by the
+  // time block g runs)
+  static constexpr int reads_after(int g) {
     int n = 0;
-    for (int t = 0; t < S::tiles(i); ++t) n += conv_block(i, t) == g;
+    for (int x = g + 1; x <= g + kPF; ++x) n += group_reads(x);
     return n;
   }
   // ---------------- compile-time vmcnt bookkeeping
-  static constexpr int tile_stores(int i) { return plane_of(i) ? (kXlo ? 2 : 1) : 0; }
+  // a mask word (8 tiles' sign bits) is stored as soon as its last tile is
+  // converted, so only one word's accumulators are live
+  static constexpr bool mask_store_at(int i, int t) {
+    return !BWD && TRAIN && S::L(i).mask >= 0 && ((t & 7) == 7 || t == S::tiles(i) - 1);
+  }
+  static constexpr int tile_stores(int i, int t) {
+    return (plane_of(i) ? (kXlo ? 2 : 1) : 0) + (mask_store_at(i, t) ? 1 : 0);
+  }
   static constexpr int final_stores(int i) {
     if (BWD) return 0;
-    const Layer l = S::L(i);
-    return (TRAIN && l.mask >= 0 ? 1 : 0) + (l.epi == EPI_SHAPE ? (TRAIN ? 2 : 1) : 0);
+    return S::L(i).epi == EPI_SHAPE ? (TRAIN ? 2 : 1) : 0;
   }
   // VMEM stores issued right after block g's MFMAs (the rgb head's come after
   // the last wait point: not counted)
   static constexpr int stores_at_block(int g) {
-    const int ci = conv_layer_at(g);
-    if (ci < 0) return 0;
-    return conv_tiles(ci, g) * tile_stores(ci) + (g == final_block(ci) ? final_stores(ci) : 0);
+    const int c = conv_at(g);
+    if (c < 0) return 0;
+    const int ci = c / 64, t = c % 64;
+    return tile_stores(ci, t) + (t == S::tiles(ci) - 1 ? final_stores(ci) : 0);
   }
   static constexpr int stores_between(int b0, int b1) {
     int s = 0;
@@ -172,7 +238,7 @@ struct Chain16 {
   }
 
   struct MaskAcc {
-    uint32_t lo[2], hi[2];
+    uint32_t lo, hi;
   };
 
   // ---------------- kernel body
@@ -184,7 +250,12 @@ struct Chain16 {
     const int m = blockIdx.x * (WAVES * kSpw) + w * kSpw + (lane & 15);
     const int mc = m < a.M ? m : a.M - 1;
     const int wg = blockIdx.x * WAVES + w;       // global 16-sample wave index
-    const int slab = wg >> 1;                    // its 32-sample plane slab
+    // its 32-sample plane slab, or -1 past the padded rows (a 12-wave
+    // workgroup's 192 samples do not divide the 256-sample pad granule):
+    // such a wave runs the schedule (barriers, weight DMA) but every store
+    // of it is discarded (empty buffer range) and it reads clamped inputs
+    const int nslab = ((a.M + 255) >> 8) << 3;
+    const int slab = (wg >> 1) < nslab ? (wg >> 1) : -1;
     const int s = 16 * (wg & 1) + (lane & 15);   // sample within the slab
     float* prm = (float*)(smem + kRingBytes);
     // per-lane byte offset of this lane's 4 features of a tile, by tile parity
@@ -197,30 +268,35 @@ struct Chain16 {
     for (int i = threadIdx.x; i < kBlobFloats / 4; i += WAVES * 64)
       ((f32x4*)prm)[i] = ((const f32x4*)a.bias)[i];
 
-    u32x4 bin[kBin];
-    u32x4 binl[kX3 ? kBin : 1];
-    f32x4 acc[16];
-    if constexpr (!BWD)
+    // the two operand arrays (hi; bf16x3 also lo) of the tile pipeline
+    u32x4 X[2][kBin];
+    u32x4 XL[2][kX3 ? kBin : 1];
+    f32x4 acc[2];
 #pragma unroll
-      for (int t = 0; t < 16; ++t) acc[t] = f32x4{};
+    for (int k = 0; k < 2; ++k) {
+      acc[k] = f32x4{};
 #pragma unroll
-    for (int u = 0; u < kBin; ++u) bin[u] = u32x4{};
-    if constexpr (kX3)
+      for (int u = 0; u < kBin; ++u) X[k][u] = u32x4{};
+      if constexpr (kX3)
 #pragma unroll
-      for (int u = 0; u < kBin; ++u) binl[u] = u32x4{};
+        for (int u = 0; u < kBin; ++u) XL[k][u] = u32x4{};
+    }
 
     float ds = 0.f;
-    if constexpr (!BWD) prologue_fwd(a, bin, binl, smem, q, lane, w, mc, slab, voff);
-    else ds = prologue_bwd(a, bin, binl, smem, q, lane, w, m, mc, wg, slab, voff);
+    if constexpr (!BWD) prologue_fwd(a, X[0], XL[0], smem, q, lane, w, mc, slab, voff);
+    else ds = prologue_bwd(a, X[0], XL[0], smem, q, lane, w, m, mc, slab >= 0 ? wg : 2 * nslab - 1, slab, voff);
     __syncthreads();
-    if constexpr (!BWD) static_for<0, S::tiles(0)>([&](auto t) { load_bias_tile<0>(acc[t], prm, q, t); });
 
     static_for<0, D>([&](auto i) { issue<i>(a, smem, w, lane); });
 
     float sig_part = 0.f;
     MaskAcc mk;
     bf16x8 Abuf[kPF + 1];
+    f32x4 Bbuf[2], Wbuf[2];         // bias tiles (by tile parity), sigma-head weights (by converted tile parity)
+    uint32_t Mbuf[2];               // mask words (by converted tile parity)
     const uint32_t lbase = lds_addr(smem) + lane * 16;
+    const uint32_t pbase = lds_addr(prm) + q * 16;    // this lane group's 4 rows of a bias / weight tile
+    const uint32_t mbase = lds_addr(smem + kMaskOff + w * kMaskWave) + lane * 8;
     auto block_off = [](int b) { return (b / kChunkBlocks % NS) * kChunkBytes + (b % kChunkBlocks) * kBlockBytes; };
     auto aread = [&](auto bbc) {
       constexpr int b = bbc;
@@ -228,6 +304,33 @@ struct Chain16 {
       u32x4 r;
       asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(lbase + (off & ~0xFFFF)), "n"(off & 0xFFFF));
       Abuf[b % (kPF + 1)] = __builtin_bit_cast(bf16x8, r);
+    };
+    auto pread = [&](f32x4& dst, auto offc) {       // 16 B of the bias blob at float offset off (+ 4 q)
+      constexpr int off = 4 * decltype(offc)::value;
+      f32x4 r;
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(pbase + (off & ~0xFFFF)), "n"(off & 0xFFFF));
+      dst = r;
+    };
+    // the side reads of group x (after its A fragment: aread)
+    auto side = [&](auto xc) {
+      constexpr int x = xc;
+      if constexpr (has_bias(x)) {
+        constexpr int li = S::layer_of(x), t = tile_of(x);
+        pread(Bbuf[t & 1], std::integral_constant<int, li * 256 + 16 * t>{});
+      }
+      constexpr int c = conv_at(x);
+      if constexpr (has_ws(x))
+        pread(Wbuf[(c % 64) & 1], std::integral_constant<int, kWsOff + 16 * (c % 64)>{});
+      if constexpr (has_mask(x)) {
+        constexpr int off = (S::L(c / 64).mask * 64) * 8 + 4 * ((c % 64) >> 3);
+        uint32_t r;
+        asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(r) : "v"(mbase), "n"(off));
+        Mbuf[(c % 64) & 1] = r;
+      }
+    };
+    auto group = [&](auto xc) {
+      aread(xc);
+      side(xc);
     };
     auto block = [&](auto gc) {
       constexpr int g = gc;
@@ -238,7 +341,7 @@ struct Chain16 {
         if constexpr (wc + D < kChunks) issue<wc + D>(a, smem, w, lane);
         if constexpr (wc == 0)
           static_for<0, kPF>([&](auto bb) {
-            if constexpr (bb < S::kBlocks) aread(bb);
+            if constexpr (bb < S::kBlocks) group(bb);
           });
       }
       constexpr int li = S::layer_of(g);
@@ -246,27 +349,45 @@ struct Chain16 {
       constexpr int t = lb / S::bpt(li);
       constexpr int kb = (lb % S::bpt(li)) / S::kAmul;
       constexpr int part = (lb % S::bpt(li)) % S::kAmul;     // bf16x3: 0 = W_hi, 1 = W_lo
-      if constexpr (g + kPF < S::kBlocks) aread(std::integral_constant<int, g + kPF>{});
-      // LDS reads return in order: wait for this block's fragment only
-      constexpr int younger = (g + kPF < S::kBlocks ? g + kPF : S::kBlocks - 1) - g;
-      asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(Abuf[g % (kPF + 1)]) : "n"(younger));
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Abuf[g % (kPF + 1)], __builtin_bit_cast(bf16x8, bin[kb]),
-                                                      (BWD && kb == 0 && part == 0) ? f32x4{} : acc[t], 0, 0, 0);
+      if constexpr (g + kPF < S::kBlocks) group(std::integral_constant<int, g + kPF>{});
+      // LDS reads return in order: wait for this block's fragment (and bias)
+      // only -- the reads of group g after them and of the later groups may
+      // still be in flight
+      constexpr int pin = li & 1;
+      constexpr bool first = !BWD && kb == 0 && part == 0;
+      constexpr int younger = reads_after(g) + has_ws(g) + has_mask(g);
+      if constexpr (first)
+        asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(Abuf[g % (kPF + 1)]), "+v"(Bbuf[t & 1]) : "n"(younger));
+      else
+        asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(Abuf[g % (kPF + 1)]) : "n"(younger));
+      f32x4& ac = acc[t & 1];
+      ac = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Abuf[g % (kPF + 1)], __builtin_bit_cast(bf16x8, X[pin][kb]),
+                                                  (BWD && kb == 0 && part == 0) ? f32x4{} : first ? Bbuf[t & 1] : ac,
+                                                  0, 0, 0);
       // bf16x3: W_hi x_lo after W_hi x_hi; the W_lo fragment multiplies x_hi
       if constexpr (kX3 && part == 0)
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Abuf[g % (kPF + 1)], __builtin_bit_cast(bf16x8, binl[kb]),
-                                                        acc[t], 0, 0, 0);
+        ac = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Abuf[g % (kPF + 1)], __builtin_bit_cast(bf16x8, XL[pin][kb]),
+                                                    ac, 0, 0, 0);
       __builtin_amdgcn_sched_barrier(kSbMask);
-      if constexpr (S::L(li).epi == EPI_RGB && g == S::last_block(li)) epilogue_rgb(a, acc, q, m);
-      constexpr int ci = conv_layer_at(g);
-      if constexpr (ci >= 0) {
-        constexpr int t0 = conv_first_tile(ci, g);
-        static_for<0, conv_tiles(ci, g)>([&](auto k) {
-          constexpr int tt = t0 + k;
-          if constexpr (!BWD) epi_tile_fwd<ci, tt>(a, bin, binl, acc, prm, q, slab, voff, sig_part, mk);
-          else epi_tile_bwd<ci, tt>(a, bin, binl, acc, prm, smem, q, lane, w, slab, voff, ds);
-        });
-        if constexpr (!BWD && g == final_block(ci)) epi_final_fwd<ci>(a, bin, binl, prm, smem, lane, w, m, wg, sig_part, mk);
+      if constexpr (S::L(li).epi == EPI_RGB && g == S::last_block(li)) epilogue_rgb(a, acc[0], q, m, slab);
+      constexpr int c = conv_at(g);
+      if constexpr (c >= 0) {
+        constexpr int ci = c / 64, tt = c % 64, po = (ci & 1) ^ 1;
+        // the side reads of group g: every read of group g before them
+        // returned, the later groups' may be in flight
+        if constexpr (has_ws(g) && has_mask(g))
+          asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(Wbuf[tt & 1]), "+v"(Mbuf[tt & 1]) : "n"(reads_after(g)));
+        else if constexpr (has_ws(g))
+          asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(Wbuf[tt & 1]) : "n"(reads_after(g)));
+        else if constexpr (has_mask(g))
+          asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(Mbuf[tt & 1]) : "n"(reads_after(g)));
+        if constexpr (!BWD) {
+          epi_tile_fwd<ci, tt>(a, X[po], XL[po], acc[tt & 1], Wbuf[tt & 1], q, lane, wg, slab, voff, sig_part, mk);
+          if constexpr (tt == S::tiles(ci) - 1)
+            epi_final_fwd<ci>(a, X[po], XL[po], prm, smem, lane, w, m, wg, slab, sig_part, mk);
+        } else {
+          epi_tile_bwd<ci, tt>(a, X[po], XL[po], acc[tt & 1], Wbuf[tt & 1], Mbuf[tt & 1], slab, voff, ds);
+        }
       }
     };
     static_for<0, kChunks>([&](auto cc) {
@@ -279,6 +400,9 @@ struct Chain16 {
 
   template <int C>
   __device__ static void issue(const ChainArgs& a, char* smem, int w, int lane) {
+    // (non-issuing waves have no LDS-DMA to wait for: their counted vmcnt
+    // waits, sized for G DMAs per chunk, only relax towards their own stores)
+    if (kIssuers < WAVES && w >= kIssuers) return;
     const auto rs = mkrsrc(a.wpack);
     const uint32_t voffs = (uint32_t)(w * G * kBlockBytes + lane * 16);
     char* dst = smem + (C % NS) * kChunkBytes + w * G * kBlockBytes;
@@ -454,9 +578,10 @@ struct Chain16 {
     return ds;
   }
 
-  // buffer descriptor of a 32-sample slab of a bf16 plane of width F
+  // buffer descriptor of a 32-sample slab of a bf16 plane of width F (slab
+  // -1: an empty range, every store discarded)
   CN_DEV static __amdgpu_buffer_rsrc_t slab_rsrc(const void* plane, int F, int slab) {
-    return mkrsrc((const char*)plane + (size_t)slab * (size_t)F * 64u);
+    return mkrsrc((const char*)plane + (size_t)(slab >= 0 ? slab : 0) * (size_t)F * 64u, slab >= 0);
   }
 
   // ---------------- epilogues
@@ -465,19 +590,27 @@ struct Chain16 {
   // Q = 2 (t & 7) + i / 2, so that ONE shift by Q brings a pair's two bits
   // to 15 and 31 (relu_mask_bf16x2, chain.hip)
   template <int LI, int TT>
-  __device__ static void epi_tile_fwd(const ChainArgs& a, u32x4* bin, u32x4* binl, f32x4* acc, const float* prm,
-                                      int q, int slab, const uint32_t* voff, float& sig_part, MaskAcc& mk) {
+  __device__ static void epi_tile_fwd(const ChainArgs& a, u32x4* bin, u32x4* binl, f32x4& ac, const f32x4& w4,
+                                      int q, int lane, int wg, int slab, const uint32_t* voff, float& sig_part,
+                                      MaskAcc& mk) {
     constexpr Layer l = S::L(LI);
     constexpr int t = TT;
-    static_assert(LI + 1 >= NL || S::tiles(LI + 1) <= S::tiles(LI), "next layer wider than this one");
-    if constexpr (t == 0) { mk.lo[0] = mk.hi[0] = mk.lo[1] = mk.hi[1] = 0u; }
-    float v0 = acc[t][0], v1 = acc[t][1], v2 = acc[t][2], v3 = acc[t][3];
+    if constexpr ((t & 7) == 0) { mk.lo = mk.hi = 0u; }
+    float v0 = ac[0], v1 = ac[1], v2 = ac[2], v3 = ac[3];
     if constexpr (TRAIN && l.mask >= 0) {
-      mk.lo[t >> 3] = push_sign(push_sign(mk.lo[t >> 3], v0), v2);
-      mk.hi[t >> 3] = push_sign(push_sign(mk.hi[t >> 3], v1), v3);
+      mk.lo = push_sign(push_sign(mk.lo, v0), v2);
+      mk.hi = push_sign(push_sign(mk.hi, v1), v3);
+    }
+    if constexpr (mask_store_at(LI, t)) {
+      // word t >> 3 of this lane's 8 B per layer (a layer of <= 8 tiles: word
+      // 1 written as 0, as one 8-B store)
+      const uint32_t mw = (mk.hi << 16) | (mk.lo & 0xFFFFu);
+      const auto rm = mkrsrc(a.masks + (size_t)wg * N::kMasks * 128, slab >= 0);
+      const uint32_t off = ((uint32_t)l.mask * 64 + lane) * 8;
+      if constexpr (S::tiles(LI) <= 8) bstore64(rm, off, u32x2{mw, 0u});
+      else bstore32(rm, off + 4 * (t >> 3), mw);
     }
     if constexpr (l.epi == EPI_SHAPE) {
-      const f32x4 w4 = *(const f32x4*)(prm + kWsOff + 16 * t + 4 * q);
       sig_part = __builtin_fmaf(w4[0], v0, sig_part);
       sig_part = __builtin_fmaf(w4[1], v1, sig_part);
       sig_part = __builtin_fmaf(w4[2], v2, sig_part);
@@ -503,28 +636,21 @@ struct Chain16 {
       if constexpr (kXlo)
         bstore64(slab_rsrc(a.Ylo[yp], N::plane_width(yp), slab), voff[t & 1], u32x2{l0, l1}, (t >> 1) * 2048);
     }
-    // this tile's accumulator starts the next layer's tile t
-    if constexpr (t < S::tiles(LI + 1)) load_bias_tile<LI + 1>(acc[t], prm, q, t);
   }
 
   template <int LI>
   __device__ static void epi_final_fwd(const ChainArgs& a, u32x4* bin, u32x4* binl, const float* prm,
-                                       const char* smem, int lane, int w, int m, int wg, float& sig_part,
-                                       MaskAcc& mk) {
+                                       const char* smem, int lane, int w, int m, int wg, int slab,
+                                       float& sig_part, MaskAcc& mk) {
     constexpr Layer l = S::L(LI);
-    if constexpr (TRAIN && l.mask >= 0) {
-      const uint32_t m0 = (mk.hi[0] << 16) | (mk.lo[0] & 0xFFFFu);
-      const uint32_t m1 = (mk.hi[1] << 16) | (mk.lo[1] & 0xFFFFu);
-      bstore64(mkrsrc(a.masks + (size_t)wg * N::kMasks * 128), ((uint32_t)l.mask * 64 + lane) * 8, u32x2{m0, m1});
-    }
     if constexpr (l.epi == EPI_SHAPE) {
       float tot = sig_part + __shfl_xor(sig_part, 16);
       tot = tot + __shfl_xor(tot, 32);
       const float pre = tot + prm[kMiscOff];
       // all four lane groups hold the full sum: every lane stores (same value,
       // same address), so the store count per wave is fixed for vmcnt
-      bstore32(mkrsrc(a.sigma), (uint32_t)m * 4, f2u(softplus20(pre)));
-      if constexpr (TRAIN) bstore32(mkrsrc(a.spre), (uint32_t)m * 4, f2u(pre));
+      bstore32(mkrsrc(a.sigma, slab >= 0), (uint32_t)m * 4, f2u(softplus20(pre)));
+      if constexpr (TRAIN) bstore32(mkrsrc(a.spre, slab >= 0), (uint32_t)m * 4, f2u(pre));
     }
     // the next layer (viewdir) takes the dir k-block from the LDS stash
     if constexpr (S::L(LI + 1).in_kind == IN_ACC_DIR) {
@@ -534,23 +660,21 @@ struct Chain16 {
     }
   }
 
-  __device__ static void epilogue_rgb(const ChainArgs& a, const f32x4* acc, int q, int m) {
-    if (q == 0) {
-      a.rgb[3 * m + 0] = acc[0][0];
-      a.rgb[3 * m + 1] = acc[0][1];
-      a.rgb[3 * m + 2] = acc[0][2];
+  __device__ static void epilogue_rgb(const ChainArgs& a, const f32x4& acc, int q, int m, int slab) {
+    if (q == 0 && slab >= 0) {
+      a.rgb[3 * m + 0] = acc[0];
+      a.rgb[3 * m + 1] = acc[1];
+      a.rgb[3 * m + 2] = acc[2];
     }
   }
 
   template <int LI, int TT>
-  __device__ static void epi_tile_bwd(const ChainArgs& a, u32x4* bin, u32x4* binl, f32x4* acc, const float* prm,
-                                      const char* smem, int q, int lane, int w, int slab, const uint32_t* voff,
-                                      float ds) {
+  __device__ static void epi_tile_bwd(const ChainArgs& a, u32x4* bin, u32x4* binl, const f32x4& ac, const f32x4& w4,
+                                      uint32_t mw, int slab, const uint32_t* voff, float ds) {
     constexpr Layer l = S::L(LI);
     constexpr int t = TT;
-    float v0 = acc[t][0], v1 = acc[t][1], v2 = acc[t][2], v3 = acc[t][3];
+    float v0 = ac[0], v1 = ac[1], v2 = ac[2], v3 = ac[3];
     if constexpr (l.epi == EPI_BSIGMA) {
-      const f32x4 w4 = *(const f32x4*)(prm + kWsOff + 16 * t + 4 * q);
       v0 = fadd_rn(v0, fmul_rn(ds, w4[0]));
       v1 = fadd_rn(v1, fmul_rn(ds, w4[1]));
       v2 = fadd_rn(v2, fmul_rn(ds, w4[2]));
@@ -560,7 +684,6 @@ struct Chain16 {
     uint32_t l0 = 0u, l1 = 0u;
     if constexpr (kX3) { l0 = resid_bf16x2(v0, v1, p0); l1 = resid_bf16x2(v2, v3, p1); }
     if constexpr (l.epi == EPI_BMASK) {
-      const uint32_t mw = *(const uint32_t*)(smem + kMaskOff + w * kMaskWave + (l.mask * 64 + lane) * 8 + 4 * (t >> 3));
       p0 = relu_mask_bf16x2<2 * (t & 7)>(p0, mw);
       p1 = relu_mask_bf16x2<2 * (t & 7) + 1>(p1, mw);
       if constexpr (kX3) {
