@@ -152,6 +152,34 @@ def test_c2_train_step_bf16_full_image():
         assert float(a16[torch.arange(n_obj) != obj].abs().max()) == 0.0      # untouched rows
     print("C2 bf16 vs fp32 gradient rel-L2, worst:", sorted(worst)[-3:])
 
+    # (2b) the HIP fp32 full-image gradients against the REFERENCE at C2 size:
+    # the oracle's fine_image_step (src/trainer.py:64-84 with the fine pass,
+    # backward per chunk) replayed in torch on the GPU in fp32 and in float64,
+    # on the same rays, z and fine samples: per tensor err(HIP fp32) <= 2
+    # err(torch fp32) + 2e-4 against float64 (test_gpu_parity.py's budget)
+    def oracle_grads(dtype):
+        pp = {k: torch.tensor(v, dtype=dtype, device=dev, requires_grad=True) for k, v in params.items()}
+        so = torch.tensor(s0, dtype=dtype, device=dev, requires_grad=True)
+        to = torch.tensor(t0, dtype=dtype, device=dev, requires_grad=True)
+        ref_cpu.fine_image_step(pp, so, to, obj, ro_d.to(dtype), vd_d.to(dtype), z.to(dev, dtype),
+                                z_f.to(dev, dtype), gt.to(dev, dtype), chunk=2048, reg_coef=1e-4)
+        return {k: v.grad for k, v in pp.items()}, so.grad[obj], to.grad[obj]
+    (o32, os32, ot32), (o64, os64, ot64) = oracle_grads(torch.float32), oracle_grads(torch.float64)
+    bad, rows = [], []
+    for k, p32 in m32.named_parameters():
+        e_ours, e_ref = _rel_l2(p32.grad, o64[k]), _rel_l2(o32[k], o64[k])
+        rows.append((e_ours, k, e_ref, _rel_l2(g16[k], o64[k])))
+        if e_ours > 2 * e_ref + 2e-4:
+            bad.append((k, e_ours, e_ref))
+    for name, ours, r32, r64 in (("shape", st32.grad[obj], os32, os64), ("texture", tt32.grad[obj], ot32, ot64)):
+        e_ours, e_ref = _rel_l2(ours, r64), _rel_l2(r32, r64)
+        rows.append((e_ours, name + "_code", e_ref, float("nan")))
+        if e_ours > 2 * e_ref + 2e-4:
+            bad.append((name, e_ours, e_ref))
+    print("C2 full-image gradients vs float64 (HIP fp32, torch fp32, HIP bf16), worst HIP fp32:",
+          [(k, f"{e:.2e}", f"{r:.2e}", f"{b:.2e}") for e, k, r, b in sorted(rows)[-4:]])
+    assert not bad, bad
+
     # (3) AdamW: the update applied to the bf16 gradients == torch AdamW order
     ref_p = {k: torch.tensor(v) for k, v in params.items()}
     for k, v in ref_p.items():
