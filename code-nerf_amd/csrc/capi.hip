@@ -293,7 +293,7 @@ static int mlp_fwd_impl(int codes, const cn_plan* p, const void* d_pack, const f
     a.pelo = L.pelo ? b + L.pelo + r0 * 64 * es : nullptr;
     for (int i = 0; i < kMaxPlanes; ++i) a.Ylo[i] = L.Ylo[i] ? b + L.Ylo[i] + r0 * L.Yw[i] * es : nullptr;
   }
-  const int grid = (Mp + p->cs.waves_fwd * p->cs.spw - 1) / (p->cs.waves_fwd * p->cs.spw);
+  const int grid = (Mp + p->cs.waves_fwd * 32 - 1) / (p->cs.waves_fwd * 32);
   launch_hot(d_act ? (codes ? p->cs.fwd_codes : p->cs.fwd_train) : p->cs.fwd_infer, dim3(grid),
              dim3(p->cs.waves_fwd * 64), S(stream), a);
   return launch_check("chain_kernel(fwd)");
@@ -347,7 +347,7 @@ static int mlp_bwd_impl(int codes, const cn_plan* p, const void* d_pack, const f
   a.d8 = b + L.d8 + r0 * 32 * es;
   a.spre = (float*)(b + L.spre) + r0;
   a.masks = (uint32_t*)(b + L.masks + (r0 / 32) * L.mask_bytes_per_slab);
-  launch_hot(codes ? p->cs.bwd_codes : p->cs.bwd, dim3((Mp + p->cs.waves_bwd * p->cs.spw - 1) / (p->cs.waves_bwd * p->cs.spw)),
+  launch_hot(codes ? p->cs.bwd_codes : p->cs.bwd, dim3((Mp + p->cs.waves_bwd * 32 - 1) / (p->cs.waves_bwd * 32)),
              dim3(p->cs.waves_bwd * 64), S(stream), a);
   return launch_check("chain_kernel(bwd)");
 }

@@ -29,7 +29,6 @@ struct ChainSet {
   int prec = 0, SB = 0, TB = 0;      // prec: plane / dW element type (0 fp32, 1 bf16)
   int x3 = 0;                         // chain kernels in bf16x3 (CN_P_BF16X3)
   int waves_fwd = 0, waves_bwd = 0;   // waves per workgroup of the forward / backward chain kernels
-  int spw = 32;                       // samples per wave (32: chain.hip; 16: chain16.hip)
   int tile = 0;                        // row alignment of a launch (the 256-sample pad granule)
   int n_params = 0, n_inject = 0, n_fwd_layers = 0;
   size_t pack_fwd_bytes = 0, pack_bwd_bytes = 0;

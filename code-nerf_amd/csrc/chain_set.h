@@ -4,7 +4,6 @@
 #pragma once
 #include <algorithm>
 #include "chain.hip"
-#include "chain16.hip"
 #include "chain_inst.h"
 #include "dw_args.h"
 #include "latent.hip"
@@ -70,54 +69,6 @@ std::vector<int32_t> build_pack_table() {
           if (kf < out_f && row < in_f) v = src_idx(l.w, kf * in_f + row);
         }
         tab[((size_t)g * 64 + lane) * EPL + e] = (v >= 0 && lo) ? (v | kPackLo) : v;
-      }
-    }
-  }
-  return tab;
-}
-
-// The same for the 16x16x32 chains (chain16.hip): block = 16 output rows x
-// 32 k-slots, lane l: row 16 t + (l & 15), k-slots 8 (l >> 4) + e.
-template <int P, int SB, int TB, bool BWD>
-std::vector<int32_t> build_pack_table16() {
-  using S = Sched16<P, SB, TB, BWD>;
-  using N = Net<SB, TB>;
-  std::vector<int32_t> tab((size_t)S::kChunks * kChunkBlocks * 64 * 8, -1);
-  for (int g = 0; g < S::kBlocks; ++g) {
-    const int li = S::layer_of(g);
-    const Layer l = S::L(li);
-    const int lb = g - S::first_block(li);
-    const int t = lb / S::bpt(li), kb = (lb % S::bpt(li)) / S::kAmul;
-    const bool lo = (lb % S::bpt(li)) % S::kAmul == 1;     // bf16x3: the W_lo fragment
-    for (int lane = 0; lane < 64; ++lane) {
-      const int q = lane >> 4;
-      const int row = 16 * t + (lane & 15);
-      for (int e = 0; e < 8; ++e) {
-        int32_t v = -1;
-        if (!BWD) {
-          const int in_real = real_in_width<SB>(li, TB);
-          const int out_real = li == N::kFwdLayers - 1 ? 3 : l.T * 32;
-          int f;
-          if (l.in_kind == IN_PE) {
-            const int c = col16(kb, q, e);
-            f = pe_slot_feature(col_half(c), col_slot(c));
-          } else if (l.in_kind == IN_ACC_DIR && kb >= 8) {
-            const int c = col16(kb - 8, q, e);
-            const int d = dir_slot_feature(col_half(c), col_slot(c));
-            f = d < 0 ? -1 : 256 + d;
-          } else {
-            f = acc16_feature(kb, q, e);
-          }
-          if (f >= 0 && f < in_real && row < out_real) v = src_idx(l.w, row * in_real + f);
-        } else {
-          // transposed: output row = forward input feature, k = forward output feature
-          const int fl = li == 0 ? N::kFwdLayers - 1 : N::kFwdLayers - 1 - li;
-          const int in_f = real_in_width<SB>(fl, TB);
-          const int out_f = fl == N::kFwdLayers - 1 ? 3 : N::fwd(fl).T * 32;
-          const int kf = acc16_feature(kb, q, e);      // li == 0: the drgb component
-          if (kf < out_f && row < in_f) v = src_idx(l.w, kf * in_f + row);
-        }
-        tab[((size_t)g * 64 + lane) * 8 + e] = (v >= 0 && lo) ? (v | kPackLo) : v;
       }
     }
   }
@@ -367,13 +318,13 @@ int db_setup(char* act, int act_M, int M, float* dbuf, char* ws, DbArgs* db) {
 template <int P, int SB, int TB>
 ChainSet make_chain_set() {
   using N = Net<SB, TB>;
-  // bf16: 8-wave workgroups of 32-sample waves (two waves per SIMD, one
-  // workgroup per CU); fp32 (bin operand of 144 VGPRs): 4 waves, one per
-  // SIMD; bf16x3: the 16x16x32 chains (chain16.hip), 8 waves of 16 samples,
-  // two per SIMD
-  constexpr bool k16 = P == CN_P_BF16X3;
-  constexpr int WF = P == CN_P_FP32 ? 4 : 8;
-  constexpr int WB = P == CN_P_FP32 ? 4 : 8;
+  // bf16: 8-wave workgroups (two waves per SIMD, one workgroup per CU) by
+  // default; fp32 (bin operand of 144 VGPRs) and bf16x3 (hi + lo operands,
+  // 2 x 72 VGPRs, beside 128 accumulator registers): 4 waves, one per SIMD
+  // (round 5 measured a 16-sample, two-waves-per-SIMD bf16x3 layout and kept
+  // this one: DESIGN.md section 7, Round 5)
+  constexpr int WF = P == CN_P_BF16 ? 8 : 4;
+  constexpr int WB = P == CN_P_BF16 ? 8 : 4;
   ChainSet s;
   s.prec = P != CN_P_FP32;     // activation-plane element type: 1 = bf16 (bf16, bf16x3)
   s.x3 = P == CN_P_BF16X3;
@@ -381,33 +332,20 @@ ChainSet make_chain_set() {
   s.TB = TB;
   s.waves_fwd = WF;
   s.waves_bwd = WB;
-  s.spw = k16 ? 16 : 32;
   s.tile = 256;
   s.n_params = ParamIdx{SB, TB}.count();
   s.n_inject = N::kInject;
   s.n_fwd_layers = N::kFwdLayers;
   s.blob_floats = BiasBlob<SB, TB>::kFloats;
-  if constexpr (k16) {
-    s.pack_fwd_bytes = Sched16<P, SB, TB, false>::packed_bytes();
-    s.pack_bwd_bytes = Sched16<P, SB, TB, true>::packed_bytes();
-    s.fwd_train = chain16_kernel<P, SB, TB, false, WF, CN_MODE_TRAIN>;
-    s.fwd_infer = chain16_kernel<P, SB, TB, false, WF, CN_MODE_INFER>;
-    s.fwd_codes = chain16_kernel<P, SB, TB, false, WF, CN_MODE_CODES>;
-    s.bwd = chain16_kernel<P, SB, TB, true, WB, CN_MODE_TRAIN>;
-    s.bwd_codes = chain16_kernel<P, SB, TB, true, WB, CN_MODE_CODES>;
-    s.fwd_table = build_pack_table16<P, SB, TB, false>;
-    s.bwd_table = build_pack_table16<P, SB, TB, true>;
-  } else {
-    s.pack_fwd_bytes = Sched<P, SB, TB, false>::packed_bytes();
-    s.pack_bwd_bytes = Sched<P, SB, TB, true>::packed_bytes();
-    s.fwd_train = chain_kernel<P, SB, TB, false, WF, CN_MODE_TRAIN>;
-    s.fwd_infer = chain_kernel<P, SB, TB, false, WF, CN_MODE_INFER>;
-    s.fwd_codes = chain_kernel<P, SB, TB, false, WF, CN_MODE_CODES>;
-    s.bwd = chain_kernel<P, SB, TB, true, WB, CN_MODE_TRAIN>;
-    s.bwd_codes = chain_kernel<P, SB, TB, true, WB, CN_MODE_CODES>;
-    s.fwd_table = build_pack_table<P, SB, TB, false>;
-    s.bwd_table = build_pack_table<P, SB, TB, true>;
-  }
+  s.pack_fwd_bytes = Sched<P, SB, TB, false>::packed_bytes();
+  s.pack_bwd_bytes = Sched<P, SB, TB, true>::packed_bytes();
+  s.fwd_train = chain_kernel<P, SB, TB, false, WF, CN_MODE_TRAIN>;
+  s.fwd_infer = chain_kernel<P, SB, TB, false, WF, CN_MODE_INFER>;
+  s.fwd_codes = chain_kernel<P, SB, TB, false, WF, CN_MODE_CODES>;
+  s.bwd = chain_kernel<P, SB, TB, true, WB, CN_MODE_TRAIN>;
+  s.bwd_codes = chain_kernel<P, SB, TB, true, WB, CN_MODE_CODES>;
+  s.fwd_table = build_pack_table<P, SB, TB, false>;
+  s.bwd_table = build_pack_table<P, SB, TB, true>;
   s.latent_fwd = latent_fwd_kernel<SB, TB>;
   s.latent_bwd = latent_bwd_kernel<SB, TB>;
   s.code_grad = code_grad_kernel<SB, TB>;

@@ -11,9 +11,10 @@ GPU (emuG) and on the CPU (emuC, a second fp32 summation order).  Per
 parameter / code tensor the kernel's distance to emuG must be of the size of
 emuG's distance to emuC: the kernel differs from its emulation by
 fp32-order noise, amplified through the bf16 roundings both apply.
-Measured round 5 (profiles/r05f/trace_seed3_k.log): ratios 0.9-1.2 on 27 of
-30 tensors, 2.6-3.7 on encoding_shape and encoding_viewdir; the emulation
-without the fold (OPS_BF16X3_DB) was 17-41x off on encoding_shape
+Measured round 5: ratios 0.9-1.7 on all 30 tensors
+(profiles/r05m/pytest_x3c32.log; a 16x16x32 layout of the same arithmetic:
+up to 4.0 on encoding_shape / encoding_viewdir, profiles/r05f/); the
+emulation without the fold (OPS_BF16X3_DB) was 17-41x off on encoding_shape
 (profiles/r05d/trace_seed3.log).
 """
 import os

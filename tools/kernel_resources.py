@@ -65,7 +65,7 @@ def spills(path=LIB):
 
 def hot(ks):
     """the hot kernels of a kernel list: chain (forward / dX) and dW"""
-    return [k for k in ks if re.search(r"chain(16)?_kernel|dw_kernel", k[0])]
+    return [k for k in ks if re.search(r"chain_kernel|dw_kernel", k[0])]
 
 
 # hot kernels the library must contain: 6 chain sets (fp32 / bf16 / bf16x3 x
