@@ -187,6 +187,23 @@ struct Chain {
   // (bf16, two waves per SIMD: the other wave hides the latency, and the
   // counted waits measured no gain there)
   static constexpr bool kAsmLds = kX3;
+  // kAsmLds backward: the ReLU mask words of a layer (4 words = one 16-B
+  // read per lane) are read by an explicit ds_read_b128 issued with the A
+  // fragment of the layer's last block, kPF blocks ahead, and counted like
+  // the fragments -- a compiler-visible read there made it wait lgkmcnt(0)
+  // (a drain of the fragment prefetch) before every tile pair's conversion
+  static constexpr int mask_read_at(int x) {
+    if (!(kAsmLds && BWD)) return -1;
+    for (int i = 0; i < S::NL; ++i)
+      if (S::L(i).epi == EPI_BMASK && S::L(i).mask >= 0 && x == S::last_block(i)) return i;
+    return -1;
+  }
+  static constexpr int group_reads(int x) { return x < 0 || x >= S::kBlocks ? 0 : 1 + (mask_read_at(x) >= 0); }
+  static constexpr int reads_after(int g) {
+    int n = 0;
+    for (int x = g + 1; x <= g + kPF; ++x) n += group_reads(x);
+    return n;
+  }
   // sched_barrier mask after each block: VALU and SALU may cross; LDS
   // reads, MFMAs and VMEM stay in program order
   static constexpr int kSbMask = 0x6;
@@ -373,6 +390,8 @@ struct Chain {
     // behind earlier MFMAs everywhere, the first blocks of a chunk included
     bf16x8 Abuf[kPF + 1];
     const uint32_t lbase = lds_addr(smem) + lane * 16;
+    u32x4 Mq = {};      // kAsmLds backward: the mask words of the layer being converted
+    const uint32_t mbase = lds_addr(smem) + (uint32_t)(kMaskOff + ((size_t)w * N::kMasks * 64 + lane) * 16);
     auto block_off = [](int b) { return (b / kChunkBlocks % NS) * kChunkBytes + (b % kChunkBlocks) * kBlockBytes; };
     auto aread = [&](auto bbc) {
       constexpr int b = bbc;
@@ -384,6 +403,12 @@ struct Chain {
         Abuf[b % (kPF + 1)] = __builtin_bit_cast(bf16x8, r);
       } else {
         Abuf[b % (kPF + 1)] = *(const bf16x8*)(smem + off + lane * 16);
+      }
+      if constexpr (mask_read_at(b) >= 0) {
+        constexpr int moff = S::L(mask_read_at(b)).mask * 1024;
+        u32x4 r;
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(mbase), "n"(moff));
+        Mq = r;
       }
     };
     auto block = [&](auto gc) {
@@ -406,8 +431,9 @@ struct Chain {
       if constexpr (kBf16) {
         if constexpr (g + kPF < S::kBlocks) aread(std::integral_constant<int, g + kPF>{});
         if constexpr (kAsmLds) {
-          // the reads issued after block g's: g + 1 .. min(g + kPF, last)
-          constexpr int younger = (g + kPF < S::kBlocks ? g + kPF : S::kBlocks - 1) - g;
+          // the reads issued after block g's fragment: its mask read, the
+          // groups g + 1 .. min(g + kPF, last)
+          constexpr int younger = reads_after(g) + (mask_read_at(g) >= 0 ? 1 : 0);
           asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(Abuf[g % (kPF + 1)]) : "n"(younger));
         }
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
@@ -430,11 +456,14 @@ struct Chain {
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[2], bin[4 * kb + 2], acc[t], 0, 0, 0);
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[3], bin[4 * kb + 3], acc[t], 0, 0, 0);
       }
+      // this layer's mask words (read with group g) before its first conversion
+      if constexpr (mask_read_at(g) >= 0)
+        asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(Mq) : "n"(reads_after(g)));
       if constexpr (!diag(li) && g == S::last_block(li)) {
         if constexpr (!BWD)
           epilogue_fwd<li>(a, bin, binl, acc, prm, smem, h, lane, w, m, wglob, voff, sig_part, mk);
         else
-          epilogue_bwd<li>(a, bin, binl, acc, prm, smem, h, lane, w, m, wglob, voff, ds);
+          epilogue_bwd<li>(a, bin, binl, acc, prm, smem, h, lane, w, m, wglob, voff, ds, Mq);
       }
       constexpr int ci = conv_layer_at(g);       // diagonal schedule: this block's tile conversions
       if constexpr (ci >= 0) {
@@ -444,7 +473,7 @@ struct Chain {
           if constexpr (!BWD)
             epi_tile_fwd<ci, tt>(a, bin, binl, acc, prm, h, wglob, voff, sig_part, mk);
           else
-            epi_tile_bwd<ci, tt>(a, bin, binl, acc, prm, smem, h, lane, w, wglob, voff, ds);
+            epi_tile_bwd<ci, tt>(a, bin, binl, acc, prm, smem, h, lane, w, wglob, voff, ds, Mq);
         });
         if constexpr (!BWD && g == final_block(ci))
           epi_final_fwd<ci>(a, bin, binl, prm, smem, lane, w, m, wglob, sig_part, mk);
@@ -807,14 +836,16 @@ struct Chain {
   template <int LI, int TT>
   __device__ static void epi_tile_bwd(const ChainArgs& a, BinT* bin, BinT* binl, f32x16* acc, const float* prm,
                                       const char* smem, int h, int lane, int w, int wglob, const uint32_t* voff,
-                                      float ds) {
+                                      float ds, const u32x4& mq) {
     constexpr Layer l = S::L(LI);
     constexpr int t = TT;
     constexpr int width = N::dplane_width(l.plane);
     const auto rdA = slab_rsrc<E>(a.dA[l.plane], width, wglob);
     uint32_t mw = 0u;     // the mask word of this tile pair
-    if constexpr (l.epi == EPI_BMASK)
-      mw = *(const uint32_t*)(smem + kMaskOff + (((size_t)w * N::kMasks + l.mask) * 64 + lane) * 16 + 4 * (t >> 1));
+    if constexpr (l.epi == EPI_BMASK) {
+      if constexpr (kAsmLds) mw = mq[t >> 1];      // read with the layer's last block (mask_read_at)
+      else mw = *(const uint32_t*)(smem + kMaskOff + (((size_t)w * N::kMasks + l.mask) * 64 + lane) * 16 + 4 * (t >> 1));
+    }
     const float* ws = prm + kWsOff + 4 * h;
     u32x2 pg[4];
 #pragma unroll
@@ -866,8 +897,10 @@ struct Chain {
   template <int LI>
   __device__ static void epilogue_bwd(const ChainArgs& a, BinT* bin, BinT* binl, f32x16* acc, const float* prm,
                                       const char* smem, int h, int lane, int w, int m, int wglob,
-                                      const uint32_t* voff, float ds) {
-    static_for<0, S::L(LI).T>([&](auto t) { epi_tile_bwd<LI, t>(a, bin, binl, acc, prm, smem, h, lane, w, wglob, voff, ds); });
+                                      const uint32_t* voff, float ds, const u32x4& mq) {
+    static_for<0, S::L(LI).T>([&](auto t) {
+      epi_tile_bwd<LI, t>(a, bin, binl, acc, prm, smem, h, lane, w, wglob, voff, ds, mq);
+    });
   }
 };
 
