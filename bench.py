@@ -42,7 +42,9 @@ FLOP_PER_SAMPLE = {"fwd": 899_328, "bwd": 853_248, "dw": 768_256}
 DW_FOLD_FLOP = 2 * 2 * 257 ** 3
 # Bytes per ray-sample the dW pass must read: the bf16 dA + X operand planes
 # the forward / dX chains stored (encoding_shape folded).
-DW_BYTES_PER_SAMPLE = {"bf16": 6_976, "bf16x3": 10_432, "fp32": 13_952}   # + the X lo planes in bf16x3
+DW_BYTES_PER_SAMPLE = {"bf16": 6_976, "bf16x3": 10_432, "bf16x3f": 6_976,
+                       "fp32": 13_952}   # + the X lo planes in bf16x3; bf16x3f's dW is the bf16 one
+PRECISIONS = ("bf16", "bf16x3", "bf16x3f", "fp32")
 KERNEL_NAMES = {"fwd": "chain_kernel<fwd,train>", "bwd": "chain_kernel<bwd>", "dw": "dw_kernel"}
 # algorithmic HBM bytes per ray of the fused ray-major step
 # (24 B origin + direction in, 12 B gt, 12 B rgb out)
@@ -62,8 +64,9 @@ def parse():
     ap.add_argument("--H", type=int, default=128)
     ap.add_argument("--n-coarse", type=int, default=64)
     ap.add_argument("--n-fine", type=int, default=64)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "bf16x3", "fp32"],
-                    help="chain arithmetic: bf16 operands | bf16x3 (hi + lo operands, 3 MFMAs per block) | fp32")
+    ap.add_argument("--precision", default="bf16", choices=list(PRECISIONS),
+                    help="chain arithmetic: bf16 operands | bf16x3 (hi + lo operands, 3 MFMAs per block) | "
+                         "bf16x3f (the bf16x3 forward, the bf16 backward) | fp32")
     ap.add_argument("--objects", type=int, default=64)
     ap.add_argument("--weights", default="weights/c2_regime_400.pth",
                     help="reference-format checkpoint (models.pth: model_params, shape/texture_code_params) to "
@@ -367,7 +370,9 @@ def main():
     timers = Timers()
     log(f"config {args.config}, precision {args.precision}, world {world}")
     wl = build_workload(args, dev, rank, world, args.precision, timers, dist)
+    clock = {"before_warmup": clock_probe(dev)}
     dt, median = timed_run(wl, args.steps, args.warmup, timers, dist, dev)
+    clock["after_timed"] = clock_probe(dev)
     samples_per_step = wl["samples_per_step"]
     value = samples_per_step * world * args.steps / dt
     ms = dt / args.steps * 1e3
@@ -380,16 +385,20 @@ def main():
     others = {}
     if args.config in ("c2", "c3") and not args.no_fp32:
         del wl
-        for prec in [p for p in ("bf16", "bf16x3", "fp32") if p != args.precision]:
+        for prec in [p for p in PRECISIONS if p != args.precision]:
             t2 = Timers()
             log(f"secondary precision {prec}")
             wl2 = build_workload(args, dev, rank, world, prec, t2, dist)
             n2 = max(5, args.steps // (5 if prec == "fp32" else 2))
             dt2, med2 = timed_run(wl2, n2, 3, t2, dist, dev)
+            ms2 = dt2 / n2 * 1e3
             others[prec] = {"value": round(samples_per_step * world * n2 / dt2, 1), "unit": "ray-samples/s",
-                            "ms_per_step": round(dt2 / n2 * 1e3, 3), "ms_per_step_median": round(med2, 3),
-                            "steps": n2, "dtype": prec}
+                            "ms_per_step": round(ms2, 3), "ms_per_step_median": round(med2, 3),
+                            "steps": n2, "dtype": prec,
+                            "roofline": roofline(args, t2, samples_per_step, ms2,
+                                                 wl2["core"].step_impl.overlap_dw, precision=prec, steps=n2)}
             del wl2
+        clock["after_secondary"] = clock_probe(dev)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -417,12 +426,39 @@ def main():
                        "name": args.config, "objects_per_step": world,
                        "rays_per_step_per_gpu": R, "parallelism": f"dp{world}"},
             "roofline": roof,
+            "clock": dict(clock, note=CLOCK_NOTE),
             "precisions": others or None,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()
+
+
+CLOCK_NOTE = ("effective shader clock of this box under a dense bf16 MFMA load (cn_clock_probe: every CU, "
+              "back-to-back v_mfma_f32_32x32x16_bf16 on hashed operands, s_memtime / s_memrealtime stamps, median "
+              "over workgroups), measured before the warm-up and after the timed steps: step times of two runs "
+              "compare at these clocks")
+
+
+def clock_probe(dev, n_wg=1024, iters=12000):
+    """cn_clock_probe on ``dev``: {"ghz", "bf16_tflops", "ms"} -- the median
+    over workgroups of stamped shader cycles / 100 MHz ticks, and the probe's
+    own MFMA rate (n_wg x 4 waves x iters x 4 MFMAs x 32,768 FLOP / wall)."""
+    import numpy as np
+    from codenerf_amd import _lib
+    L = _lib.lib()
+    out = torch.zeros(3 * n_wg, dtype=torch.int32, device=dev)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    _lib.check(L.cn_clock_probe(_lib.ptr(out), n_wg, iters, 12345, _lib.stream_ptr(dev)), "cn_clock_probe")
+    b.record()
+    torch.cuda.synchronize(dev)
+    o = out.cpu().numpy().view(np.uint32).reshape(-1, 3).astype(np.float64)
+    ghz = float(np.median(o[:, 0] / np.maximum(o[:, 1], 1))) * 0.1
+    ms = a.elapsed_time(b)
+    tf = n_wg * 4 * iters * 4 * 32768 / (ms * 1e-3) / 1e12
+    return {"ghz": round(ghz, 4), "bf16_tflops": round(tf, 1), "ms": round(ms, 3)}
 
 
 def kernel_roofline(k, precision, timers, traffic):
@@ -462,7 +498,7 @@ def kernel_roofline(k, precision, timers, traffic):
     else:
         out.update(bound="mfma", achieved=round(tf, 2), peak=peak_tf, unit="TFLOP/s", frac=round(tf / peak_tf, 4),
                    flop_per_sample=FLOP_PER_SAMPLE[k])
-        if precision == "bf16x3":
+        if precision == "bf16x3" or (precision == "bf16x3f" and k == "fwd"):
             # three bf16 MFMAs per algorithmic block: the matrix cores' own load
             out["mfma_issued"] = {"achieved": round(3 * tf, 2), "frac": round(3 * tf / peak_tf, 4),
                                   "note": "3 bf16 MFMAs (hi*hi, hi*lo, lo*hi) per algorithmic MFMA"}
@@ -474,20 +510,23 @@ def kernel_roofline(k, precision, timers, traffic):
     return out
 
 
-def roofline(args, timers, samples_per_step, ms, overlapped):
+def roofline(args, timers, samples_per_step, ms, overlapped, precision=None, steps=None):
     """Per-kernel rooflines (fwd and dX chains: MFMA; dW: HBM) and the
     dominant kernel -- the class with the most measured time per step --
-    lifted to the top level (bound / achieved / peak / unit / frac / traffic)."""
+    lifted to the top level (bound / achieved / peak / unit / frac / traffic).
+    precision / steps: those of this timed run (default: the headline's)."""
+    precision = precision or args.precision
+    steps = steps or args.steps
     summ = timers.summary()
     if not summ:
         return None
-    per_step = {k: v[1] / args.steps for k, v in summ.items()}    # ms per step (all launches)
-    launches = {k: len(timers.ev[k]) / args.steps for k in timers.ev}
+    per_step = {k: v[1] / steps for k, v in summ.items()}    # ms per step (all launches)
+    launches = {k: len(timers.ev[k]) / steps for k in timers.ev}
     passes = {"c4": ("fwd", "bwd"), "c4eval": ("fwd",)}.get(args.config, ("fwd", "bwd", "dw"))
     kinds = [k for k in FLOP_PER_SAMPLE if k in summ and k in passes]
     kernels = {}
     for k in kinds:
-        r = kernel_roofline(k, args.precision, timers, load_traffic(args.config, k, args.precision))
+        r = kernel_roofline(k, precision, timers, load_traffic(args.config, k, precision))
         if r is not None:
             if args.config == "c4eval":
                 r["kernel"] = "chain_kernel<fwd,infer>"
@@ -506,7 +545,7 @@ def roofline(args, timers, samples_per_step, ms, overlapped):
     if overlapped and "dw" in passes:
         roof["overlap"] = ("dX chain of row range i on the main stream || dW of range i-1 on a side stream; "
                            "per-kernel spans overlap, so their sum exceeds the step")
-    peak = FP32_PEAK_TFLOPS if args.precision == "fp32" else BF16_PEAK_TFLOPS
+    peak = FP32_PEAK_TFLOPS if precision == "fp32" else BF16_PEAK_TFLOPS
     # SURVEY.md 8(d)'s algorithmic view of the dominant kernel, beside the
     # operand-byte / counter-byte view above: its algorithmic FLOPs against
     # the MFMA peak, and its counted HBM bytes against the step's algorithmic

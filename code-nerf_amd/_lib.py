@@ -22,6 +22,7 @@ ABI_VERSION = 3
 CN_FP32 = 0
 CN_BF16 = 1
 CN_BF16X3 = 2
+CN_BF16X3F = 3      # bf16x3 forward chains, bf16 backward (include/codenerf.h)
 
 
 class HipUnavailable(RuntimeError):
@@ -76,6 +77,7 @@ _SIGS = {
                                  _P]),
     "cn_adamw_step": (_I, [_I, _P, _P, _P, _P, _P, _P, _D, _D, _D, _D, _I, _P]),
     "cn_adamw_step_zero_grad": (_I, [_I, _P, _P, _P, _P, _P, _P, _D, _D, _D, _D, _I, _P]),
+    "cn_clock_probe": (_I, [_P, _I, _I, ctypes.c_uint, _P]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -14,6 +14,7 @@
 #include "dw.hip"
 #include "optim.hip"
 #include "render.hip"
+#include "probe.hip"
 
 using namespace cn;
 
@@ -118,13 +119,15 @@ int cn_plan_create(int shape_blocks, int texture_blocks, int W, int num_xyz_freq
   *out = nullptr;
   if (W != 256 || latent_dim != 256 || num_xyz_freq != 10 || num_dir_freq != 4)
     return fail("cn_plan_create: unsupported net (need W=latent_dim=256, num_xyz_freq=10, num_dir_freq=4)");
-  if (precision != CN_FP32 && precision != CN_BF16 && precision != CN_BF16X3)
-    return fail("cn_plan_create: precision must be CN_FP32, CN_BF16 or CN_BF16X3");
+  if (precision != CN_FP32 && precision != CN_BF16 && precision != CN_BF16X3 && precision != CN_BF16X3F)
+    return fail("cn_plan_create: precision must be CN_FP32, CN_BF16, CN_BF16X3 or CN_BF16X3F");
   ChainSet cs;
   if (shape_blocks == 3 && texture_blocks == 1)
-    cs = precision == CN_BF16X3 ? chain_set_bf16x3_3_1() : precision ? chain_set_bf16_3_1() : chain_set_fp32_3_1();
+    cs = precision == CN_BF16X3F ? chain_set_bf16x3f_3_1() : precision == CN_BF16X3 ? chain_set_bf16x3_3_1()
+       : precision ? chain_set_bf16_3_1() : chain_set_fp32_3_1();
   else if (shape_blocks == 2 && texture_blocks == 1)
-    cs = precision == CN_BF16X3 ? chain_set_bf16x3_2_1() : precision ? chain_set_bf16_2_1() : chain_set_fp32_2_1();
+    cs = precision == CN_BF16X3F ? chain_set_bf16x3f_2_1() : precision == CN_BF16X3 ? chain_set_bf16x3_2_1()
+       : precision ? chain_set_bf16_2_1() : chain_set_fp32_2_1();
   else return fail("cn_plan_create: unsupported (shape_blocks, texture_blocks); built: (3,1), (2,1)");
   cn_plan* p = new cn_plan();
   p->cs = cs;
@@ -571,6 +574,12 @@ int cn_adamw_step_zero_grad(int nseg, float* const* p, float* const* g, float* c
                             const int* n, const double* lr, double wd, double beta1, double beta2, double eps,
                             int step, void* stream) {
   return adamw_impl(nseg, p, g, m, v, n, lr, wd, beta1, beta2, eps, step, 1, stream);
+}
+
+int cn_clock_probe(unsigned int* d_out, int n_workgroups, int iters, unsigned int seed, void* stream) {
+  if (!d_out || n_workgroups <= 0 || iters <= 0) return fail("cn_clock_probe: bad argument");
+  hipLaunchKernelGGL(clock_probe_kernel, dim3(n_workgroups), dim3(kProbeWaves * 64), 0, S(stream), d_out, iters, seed);
+  return launch_check("clock_probe_kernel");
 }
 
 }  // extern "C"

@@ -20,6 +20,7 @@
 //     into the layer epilogues; for training the epilogues also write the
 //     layer outputs (for dW) and one sign bit per pre-activation (ReLU mask
 //     for the dX chain) with a single v_alignbit per value.
+#pragma once
 #include "cn_common.h"
 #include "cn_sched.h"
 #include "chain_args.h"
@@ -156,11 +157,13 @@ struct Chain {
   static constexpr bool kBf16 = (P != CN_P_FP32);
   static constexpr bool kX3 = (P == CN_P_BF16X3);    // hi + lo operands, three MFMAs per block
   static constexpr bool TRAIN = MODE != CN_MODE_INFER;    // masks + sigma pre-activation
-  static constexpr bool PLANES = MODE == CN_MODE_TRAIN;   // every operand plane of dW
+  // every operand plane of dW (TRAIN_HI: the bf16x3 forward of a bf16x3f plan)
+  static constexpr bool PLANES = MODE == CN_MODE_TRAIN || MODE == CN_MODE_TRAIN_HI;
   // bf16x3 training forward: also the lo parts of dW's X operands (PE and
   // every stored Y plane, from the binl registers the epilogues already
   // hold), so the weight gradients multiply hi + lo (dw.hip DwBody<..., LO>)
-  static constexpr bool kXlo = kX3 && PLANES && !BWD;
+  static constexpr bool kXlo = kX3 && MODE == CN_MODE_TRAIN && !BWD;
+  static_assert(MODE != CN_MODE_TRAIN_HI || (kX3 && !BWD), "TRAIN_HI is the bf16x3 forward of a bf16x3f plan");
   static constexpr int NL = S::NL;
   static constexpr int kChunks = S::kChunks;
   // waves that issue the weight stream's LDS-DMA (all of them when WAVES
@@ -199,6 +202,22 @@ struct Chain {
     return -1;
   }
   static constexpr int group_reads(int x) { return x < 0 || x >= S::kBlocks ? 0 : 1 + (mask_read_at(x) >= 0); }
+  // One Mq register set serves every masked layer: layer j's read (issued
+  // with block last_block(j) - kPF, before that block's conversions)
+  // overwrites it, so every earlier masked layer must have finished its
+  // conversions (final_block: its last diagonal tile) before that block.
+  static constexpr bool mask_reads_ordered() {
+    if (!(kAsmLds && BWD)) return true;
+    for (int j = 0; j < S::NL; ++j) {
+      if (mask_read_at(S::last_block(j)) != j) continue;
+      for (int i = 0; i < j; ++i) {
+        if (mask_read_at(S::last_block(i)) != i) continue;
+        const int last_use = diag(i) ? final_block(i) : S::last_block(i);
+        if (!(last_use < S::last_block(j) - kPF)) return false;
+      }
+    }
+    return true;
+  }
   static constexpr int reads_after(int g) {
     int n = 0;
     for (int x = g + 1; x <= g + kPF; ++x) n += group_reads(x);
@@ -343,6 +362,8 @@ struct Chain {
 
   // ---------------- kernel body
   __device__ static void run(const ChainArgs& a) {
+    static_assert(mask_reads_ordered(), "a masked layer's mask read would overwrite Mq before an earlier layer's "
+                                        "last conversion: double-buffer Mq or move the read");
     __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -388,7 +409,7 @@ struct Chain {
     // bf16: A fragments are read kPF blocks ahead of their MFMA (rolling
     // register buffer) across chunk boundaries, so the LDS latency hides
     // behind earlier MFMAs everywhere, the first blocks of a chunk included
-    bf16x8 Abuf[kPF + 1];
+    u32x4 Abuf[kPF + 1];      // A fragments (8 bf16 each), as the asm reads write them
     const uint32_t lbase = lds_addr(smem) + lane * 16;
     u32x4 Mq = {};      // kAsmLds backward: the mask words of the layer being converted
     const uint32_t mbase = lds_addr(smem) + (uint32_t)(kMaskOff + ((size_t)w * N::kMasks * 64 + lane) * 16);
@@ -397,18 +418,21 @@ struct Chain {
       constexpr int b = bbc;
       constexpr int off = block_off(b);
       // ds_read offsets are 16-bit: the ring's upper 64 KiB through a second base
+      // (the asm reads write their consumer's registers directly: a copy of
+      // a register whose LDS load is still in flight would read it early)
       if constexpr (kAsmLds) {
-        u32x4 r;
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(lbase + (off & ~0xFFFF)), "n"(off & 0xFFFF));
-        Abuf[b % (kPF + 1)] = __builtin_bit_cast(bf16x8, r);
+        asm volatile("ds_read_b128 %0, %1 offset:%2"
+                     : "=v"(Abuf[b % (kPF + 1)]) : "v"(lbase + (off & ~0xFFFF)), "n"(off & 0xFFFF));
       } else {
-        Abuf[b % (kPF + 1)] = *(const bf16x8*)(smem + off + lane * 16);
+        Abuf[b % (kPF + 1)] = *(const u32x4*)(smem + off + lane * 16);
       }
       if constexpr (mask_read_at(b) >= 0) {
         constexpr int moff = S::L(mask_read_at(b)).mask * 1024;
-        u32x4 r;
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(mbase), "n"(moff));
-        Mq = r;
+        // (named first: clang captures no variable of a generic lambda that
+        // only an asm operand uses)
+        u32x4& mq = Mq;
+        const uint32_t mb = mbase;
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(mq) : "v"(mb), "n"(moff));
       }
     };
     auto block = [&](auto gc) {
@@ -436,14 +460,13 @@ struct Chain {
           constexpr int younger = reads_after(g) + (mask_read_at(g) >= 0 ? 1 : 0);
           asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(Abuf[g % (kPF + 1)]) : "n"(younger));
         }
+        const bf16x8 A = __builtin_bit_cast(bf16x8, Abuf[g % (kPF + 1)]);
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-            Abuf[g % (kPF + 1)], __builtin_bit_cast(bf16x8, bin[kb]),
-            (BWD && kb == 0 && part == 0) ? f32x16{} : acc[t], 0, 0, 0);
+            A, __builtin_bit_cast(bf16x8, bin[kb]), (BWD && kb == 0 && part == 0) ? f32x16{} : acc[t], 0, 0, 0);
         // bf16x3: W_hi x_lo after W_hi x_hi (same A fragment); the W_lo
         // fragment (part 1) multiplies x_hi only
         if constexpr (kX3 && part == 0)
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Abuf[g % (kPF + 1)],
-                                                           __builtin_bit_cast(bf16x8, binl[kb]), acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, __builtin_bit_cast(bf16x8, binl[kb]), acc[t], 0, 0, 0);
         // pin the (A-fragment read, MFMA) order: left alone, the machine
         // scheduler sinks each LDS read next to its MFMA (2 buffers, a
         // lgkmcnt(0) every other MFMA), exposing the LDS latency kPF hides

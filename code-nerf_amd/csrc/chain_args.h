@@ -14,6 +14,8 @@ enum ChainMode : int {
   CN_MODE_CODES = 2,   // codes-only optimisation (src/optimizer.py): forward stores
                        // ReLU masks + sigma pre-activations, backward only the dA
                        // planes of the layers fed by a code (the bias sums need them)
+  CN_MODE_TRAIN_HI = 3,  // bf16x3 forward, training: every plane of CN_MODE_TRAIN but
+                         // not the X lo planes (CN_P_BF16X3F: a bf16 dW reads hi only)
 };
 
 // Per-call bias blob (written by the latent kernel, read by the forward chain):

@@ -60,5 +60,7 @@ ChainSet chain_set_fp32_2_1();
 ChainSet chain_set_bf16_2_1();
 ChainSet chain_set_bf16x3_3_1();
 ChainSet chain_set_bf16x3_2_1();
+ChainSet chain_set_bf16x3f_3_1();
+ChainSet chain_set_bf16x3f_2_1();
 
 }  // namespace cn

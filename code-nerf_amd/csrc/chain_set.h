@@ -4,6 +4,7 @@
 #pragma once
 #include <algorithm>
 #include "chain.hip"
+#include "chain_extern.h"
 #include "chain_inst.h"
 #include "dw_args.h"
 #include "latent.hip"
@@ -354,6 +355,48 @@ ChainSet make_chain_set() {
   s.dw_ws_bytes = dw_ws_bytes<P, SB, TB>;
   s.fold_args = fold_args<SB, TB>;
   s.db_setup = db_setup<P, SB, TB>;
+  return s;
+}
+
+// CN_P_BF16X3F: the bf16x3 forward chains (rgb within ~5e-7 of the fp32
+// reference) with the CN_P_BF16 backward: the training forward stores the hi
+// planes only (CN_MODE_TRAIN_HI -- exactly the bf16 plan's planes: the same
+// layout, masks and rounding rn(x)), which the bf16 dX chain (8 waves) and the
+// bf16 dW pass read.  Weight packs: forward = bf16x3 (W_hi, W_lo fragments),
+// backward = bf16.
+template <int SB, int TB>
+ChainSet make_chain_set_x3f() {
+  using N = Net<SB, TB>;
+  constexpr int X3 = CN_P_BF16X3, B16 = CN_P_BF16;
+  ChainSet s;
+  s.prec = 1;                 // bf16 planes and dW
+  s.x3 = 1;                   // forward chains in bf16x3
+  s.SB = SB;
+  s.TB = TB;
+  s.waves_fwd = 4;            // as the bf16x3 plan
+  s.waves_bwd = 8;            // as the bf16 plan
+  s.tile = 256;
+  s.n_params = ParamIdx{SB, TB}.count();
+  s.n_inject = N::kInject;
+  s.n_fwd_layers = N::kFwdLayers;
+  s.blob_floats = BiasBlob<SB, TB>::kFloats;
+  s.pack_fwd_bytes = Sched<X3, SB, TB, false>::packed_bytes();
+  s.pack_bwd_bytes = Sched<B16, SB, TB, true>::packed_bytes();
+  s.fwd_train = chain_kernel<X3, SB, TB, false, 4, CN_MODE_TRAIN_HI>;
+  s.fwd_infer = chain_kernel<X3, SB, TB, false, 4, CN_MODE_INFER>;
+  s.fwd_codes = chain_kernel<X3, SB, TB, false, 4, CN_MODE_CODES>;
+  s.bwd = chain_kernel<B16, SB, TB, true, 8, CN_MODE_TRAIN>;
+  s.bwd_codes = chain_kernel<B16, SB, TB, true, 8, CN_MODE_CODES>;
+  s.fwd_table = build_pack_table<X3, SB, TB, false>;
+  s.bwd_table = build_pack_table<B16, SB, TB, true>;
+  s.latent_fwd = latent_fwd_kernel<SB, TB>;
+  s.latent_bwd = latent_bwd_kernel<SB, TB>;
+  s.code_grad = code_grad_kernel<SB, TB>;
+  s.layout = act_layout<B16, SB, TB>;
+  s.dw_setup = dw_setup<B16, SB, TB>;
+  s.dw_ws_bytes = dw_ws_bytes<B16, SB, TB>;
+  s.fold_args = fold_args<SB, TB>;
+  s.db_setup = db_setup<B16, SB, TB>;
   return s;
 }
 

@@ -22,7 +22,11 @@ typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
 // into one fp32 accumulator: A_hi B_hi + A_hi B_lo + A_lo B_hi (the lo x lo
 // term, ~2^-16 relative, is dropped).  Activation planes (the dW operands)
 // are stored as in CN_P_BF16.
-enum { CN_P_FP32 = 0, CN_P_BF16 = 1, CN_P_BF16X3 = 2 };
+// CN_P_BF16X3F (a plan, not a kernel arithmetic): the bf16x3 forward chain
+// (rendered rgb at fp32 class) feeding the CN_P_BF16 backward -- dX chain and
+// dW pass on bf16 operands; the forward stores the hi planes only
+// (CN_MODE_TRAIN_HI), which are the CN_P_BF16 planes' format.
+enum { CN_P_FP32 = 0, CN_P_BF16 = 1, CN_P_BF16X3 = 2, CN_P_BF16X3F = 3 };
 
 // Compile-time for loop: f(std::integral_constant<int, I>) for I in [0, N).
 // Recursive on purpose: every level is a forceinline function, so the chain

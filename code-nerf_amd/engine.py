@@ -14,7 +14,7 @@ from torch.autograd.graph import increment_version
 from . import _lib
 from ._lib import check, ptr
 
-PRECISIONS = {"fp32": _lib.CN_FP32, "bf16": _lib.CN_BF16, "bf16x3": _lib.CN_BF16X3}
+PRECISIONS = {"fp32": _lib.CN_FP32, "bf16": _lib.CN_BF16, "bf16x3": _lib.CN_BF16X3, "bf16x3f": _lib.CN_BF16X3F}
 # Training-workspace budget per call (bytes): larger images are rendered in
 # ray parts that fit it (render.ImageStep, model.CodeNeRF.forward).  At the
 # srncar net one training sample holds ~8.2 KB (bf16) / ~16 KB (fp32) of

@@ -27,8 +27,12 @@ class CodeNeRF(nn.Module):
     """Code-conditioned NeRF MLP (reference src/model.py:10-34).
 
     Extra keyword ``precision`` selects the kernel arithmetic: "fp32" (exact
-    fp32 MFMA, parity with the reference) or "bf16" (bf16 operands, fp32
-    accumulation, throughput).
+    fp32 MFMA, parity with the reference), "bf16" (bf16 operands, fp32
+    accumulation, throughput), "bf16x3" (every chain operand and weight as a
+    bf16 hi + lo pair, three MFMAs per block; dW on hi + lo X operands) or
+    "bf16x3f" (the bf16x3 forward -- rendered rgb at fp32 class -- with the
+    bf16 backward).
+
     """
 
     def __init__(self, shape_blocks=2, texture_blocks=1, W=256, num_xyz_freq=10, num_dir_freq=4,

@@ -37,6 +37,10 @@ extern "C" {
 /* error-compensated bf16: weights and chain operands as bf16 hi + lo pairs,
  * three MFMAs per block into fp32 (~16-bit operands); dW as CN_BF16 */
 #define CN_BF16X3 2
+/* the CN_BF16X3 forward chains (rendered rgb at fp32 class) with the CN_BF16
+ * backward (dX chain and dW on bf16 operands); the training forward stores the
+ * CN_BF16 planes (hi parts only) */
+#define CN_BF16X3F 3
 /* Largest sample count (M, act_M, R * N) one call accepts: the kernels index
  * samples with 32-bit integers (3 m, 4 m).  Larger images are rendered in
  * ray parts (codenerf_amd.render.ImageStep / CodeNeRF.forward split
@@ -64,6 +68,15 @@ int cn_time_next_launch(void *start_event, void *stop_event);
  * pipelining of one step (render.ImageStep); host-visible results still need
  * the stream's own synchronisation. */
 int cn_stream_wait(void *waiter_stream, void *signaller_stream);
+
+/* Clock probe (measurement only, no reference counterpart): n_workgroups
+ * workgroups of 4 waves issue `iters` x 4 back-to-back bf16 MFMAs
+ * (v_mfma_f32_32x32x16_bf16) on hashed operands; wave 0 of each stamps the
+ * shader-cycle counter and the 100 MHz real-time counter around the loop:
+ * d_out[3 g + 0] = cycles, [3 g + 1] = 100 MHz ticks, [3 g + 2] = a checksum.
+ * Effective clock = cycles / ticks x 100 MHz (bench.py records it beside a
+ * step time, so box-to-box clock differences can be told from regressions). */
+int cn_clock_probe(unsigned int *d_out, int n_workgroups, int iters, unsigned int seed, void *stream);
 
 /* ---- plan: static layout for one network configuration and precision.
  * Replaces CodeNeRF.__init__ (src/model.py:11-34).  Creating a plan and the

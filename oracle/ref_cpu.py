@@ -107,6 +107,10 @@ OPS_BF16X3_DB = dict(OPS_BF16X3, inj_dy="b")
 # and ``fold`` -- encoding_shape / sigma / encoding_viewdir as the dW pass
 # forms their gradients through the encoding_shape fold (_FoldBlock)
 OPS_BF16X3_K = dict(OPS_BF16X3_DB, x3=True, fold=True)
+# the bf16x3f plan (precision "bf16x3f"): the bf16x3 forward chains (weights
+# and layer inputs split, three products) and the bf16 backward (dX and dW on
+# bf16 operands, the latent path from the bf16 dA sums)
+OPS_BF16X3F = dict(_OPS_BF16, fw_w="s", fw_x="s", x3=True, inj_dy="b")
 # the built kernels' per-layer exception: encoding_viewdir's dir-PE columns
 # stay hi only in dW (``bf16_operands(ops=..., layer_ops=X3_LAYER_OPS)``)
 X3_LAYER_OPS = {"encoding_viewdir.0": {"dw_x_split_cols": 256}}
@@ -237,11 +241,19 @@ class _FoldBlock(torch.autograd.Function):
         dys = _mm(dye, oe["bw_dy"], We, oe["bw_w"], oe)
         rA = _q(dvpre, ov["dw_dy"]).reshape(-1, dvpre.shape[-1])
         ysx = _q(ys, oe["dw_x"]).reshape(-1, ys.shape[-1])
-        dsf = _q(dspre, "s").reshape(-1, 1)
+        # the sigma-head gradient rides in the viewdir dA plane as value +
+        # rounding residual (chain.hip prologue_bwd): split wherever that
+        # plane is rounded, exact in an fp32 plan
+        dsf = _q(dspre, "f" if ov["dw_dy"] == "f" else "s").reshape(-1, 1)
+        # the dir-PE columns of encoding_viewdir's dW operand: dw_x, unless the
+        # layer splits only its leading dw_x_split_cols columns (X3_LAYER_OPS:
+        # the kernels keep the dir-PE tile hi only) -- then bf16
+        n_split = ov.get("dw_x_split_cols")
+        how_pe = ov["dw_x"] if n_split is None or n_split > F0 else "b"
         Gx, Gb = rA.t() @ ysx, rA.sum(0)
         Gs, Gsb = dsf.t() @ ysx, dsf.sum(0)
         dWv = torch.cat([Gx @ We.t() + Gb[:, None] * be[None, :],
-                         rA.t() @ _q(dpe, "b").reshape(-1, dpe.shape[-1])], 1)
+                         rA.t() @ _q(dpe, how_pe).reshape(-1, dpe.shape[-1])], 1)
         dWs = Gs @ We.t() + Gsb[:, None] * be[None, :]
         dWe = Wv[:, :F0].t() @ Gx + Ws.t() @ Gs
         dbe = Wv[:, :F0].t() @ Gb + Ws[0] * Gsb
@@ -300,6 +312,8 @@ def codenerf_forward(p, xyz, viewdir, shape_code, texture_code, shape_blocks=3,
         h = F.relu(_lin_inj(p, f"shape_layer_{j}.0", h, z))
         if acts is not None:
             acts[f"y{j}"] = h
+    # (the fold computes encoding_shape's output inside _FoldBlock: a call
+    # asking for the per-layer activations runs the per-layer restatement)
     if _BF16["on"] and _BF16["ops"].get("fold") and acts is None:
         lo = _BF16.get("layer_ops", {})
         dpe = positional_encoding(viewdir, num_dir_freq)

@@ -76,6 +76,37 @@ def test_plan_and_size_queries_need_no_device():
         lib.cn_plan_destroy(h)
 
 
+def test_bf16x3f_plan_composes_the_bf16x3_forward_and_the_bf16_backward():
+    """CN_BF16X3F: the forward pack of the bf16x3 plan (W_hi + W_lo
+    fragments), the backward pack and the workspace of the bf16 plan (its
+    training forward stores the bf16 planes only); bf16x3's workspace is the
+    same layout with the X lo planes appended."""
+    import codenerf_amd._lib as L
+    if not os.path.exists(L.LIB_PATH):
+        pytest.skip("library not built")
+    lib = L.load_library()
+    h16, h3, h3f = _plan(lib, L.CN_BF16), _plan(lib, L.CN_BF16X3), _plan(lib, L.CN_BF16X3F)
+    assert lib.cn_packed_bytes(h3f, 0) == lib.cn_packed_bytes(h3, 0) > lib.cn_packed_bytes(h16, 0)
+    assert lib.cn_packed_bytes(h3f, 1) == lib.cn_packed_bytes(h16, 1)
+    M = 4133
+    assert lib.cn_act_bytes(h3f, M) == lib.cn_act_bytes(h16, M) < lib.cn_act_bytes(h3, M)
+    import ctypes
+    for kind, idx in ((L_PLANE_Y, 1), (L_PLANE_DA, 2), (L_PLANE_PE, 0), (L_PLANE_MASKS, 0)):
+        w3f, w3 = ctypes.c_int(), ctypes.c_int()
+        o3f = lib.cn_act_plane(h3f, M, kind, idx, ctypes.byref(w3f))
+        o3 = lib.cn_act_plane(h3, M, kind, idx, ctypes.byref(w3))
+        assert o3f == o3 >= 0 and w3f.value == w3.value
+    assert lib.cn_act_plane(h3f, M, L_PLANE_PELO, 0, None) == -1
+    assert lib.cn_act_plane(h3, M, L_PLANE_PELO, 0, None) > 0
+    for h in (h16, h3, h3f):
+        lib.cn_plan_destroy(h)
+    bad = ctypes.c_void_p()
+    assert lib.cn_plan_create(3, 1, 256, 10, 4, 256, 4, ctypes.byref(bad)) == -1
+
+
+L_PLANE_Y, L_PLANE_DA, L_PLANE_PE, L_PLANE_MASKS, L_PLANE_PELO = 0, 1, 2, 4, 6     # include/codenerf.h
+
+
 @pytest.mark.parametrize("fn", ["cn_mlp_fwd", "cn_mlp_bwd", "cn_mlp_dw"])
 def test_sample_guard_rejects_oversized_calls(fn):
     """A call over CN_MAX_SAMPLES samples fails with -1 and a message before

@@ -31,9 +31,9 @@ meaningful, and convergence separately:
    the bf16 operand precision of the C2 config, not the kernels -- printed,
    not asserted.  bf16x3 against the fp32 replay: leaves 0.05 dB at step 19
    (0.09 dB; round 4) where the reference computed on the GPU stays within
-   0.025 dB of the CPU one for 29 steps: asserted over the first 18 steps,
-   and against the replay of its OWN arithmetic (ref_cpu.OPS_BF16X3_K) over
-   its replayable prefix (>= 15 steps).
+   0.025 dB of the CPU one for 29 steps: the bar over the reference's own
+   horizon is asserted as an expected failure
+   (test_early_bf16x3_over_the_reference_horizon).
 2. CONVERGENCE over ITERS steps for several initialisations: fp32 and bf16
    both exceed 20 dB (best 50-step mean).  The bf16 - fp32 gap of the final
    100-step means is printed next to the gap between two fp32 summation
@@ -51,8 +51,11 @@ pytestmark = pytest.mark.gpu
 ITERS, EARLY, TAIL = 900, 30, 100
 SEEDS = (0, 2)              # seed 1 plateaus at 18.8 dB in both precisions within ITERS
 BF16_TAIL_DB = 1.0          # bar on |bf16 - fp32| tail gaps (measured round 3: 0.748 / 0.063 dB; two fp32 orders: 0.402)
-X3_FP32_STEPS = 18          # bf16x3 within 0.05 dB of the fp32 replay over these steps (first exit round 4: 19)
-X3_PREFIX = 15              # bf16x3 within 0.05 dB of its own arithmetic's replay at least this long
+# bf16x3's bars in this regime are the reference's own: over the HORIZON in
+# which the reference computed by a second fp32 implementation (torch on the
+# GPU) stays within half the bar (0.025 dB) of the CPU replay, bf16x3 within
+# 0.05 dB of the fp32 replay and of the replay of its own arithmetic
+# (test_early_bf16x3_over_the_reference_horizon: an expected failure, see there)
 
 
 
@@ -118,15 +121,32 @@ def _replay(root, init, seed, steps, bf16, x3=False):
     return np.array(ps)
 
 
+_EARLY = {}
+
+
+def _early_runs(tmp_path):
+    """The EARLY-step runs of seed 0 (shared by the two early tests)."""
+    if not _EARLY:
+        root = _data(tmp_path)
+        A, init = _run(tmp_path, root, "A", "fp32", True, 0, EARLY)
+        H, _ = _run(tmp_path, root, "bf16", "bf16", True, 0, EARLY, init)
+        X, _ = _run(tmp_path, root, "bf16x3", "bf16x3", True, 0, EARLY, init)
+        XF, _ = _run(tmp_path, root, "bf16x3f", "bf16x3f", True, 0, EARLY, init)
+        ref32 = _replay(root, init, 0, EARLY, bf16=False)
+        ref16 = _replay(root, init, 0, EARLY, bf16=True)
+        refx3 = _replay(root, init, 0, EARLY, bf16=True, x3=True)
+        from test_gpu_train import _oracle_training
+        torch.manual_seed(1000)
+        np.random.seed(1000)
+        refg = np.array(_oracle_training(_hp(root, "fp32"), init, EARLY, 256, device="cuda")[0])
+        _EARLY.update(A=A, H=H, X=X, XF=XF, ref32=ref32, ref16=ref16, refx3=refx3, refg=refg)
+    return _EARLY
+
+
 @pytest.mark.timeout(600)
 def test_early_train_psnr_matches_reference_at_each_precision(tmp_path):
-    root = _data(tmp_path)
-    A, init = _run(tmp_path, root, "A", "fp32", True, 0, EARLY)
-    B, _ = _run(tmp_path, root, "B", "fp32", False, 0, EARLY, init)      # a second fp32 summation order
-    H, _ = _run(tmp_path, root, "bf16", "bf16", True, 0, EARLY, init)
-    X, _ = _run(tmp_path, root, "bf16x3", "bf16x3", True, 0, EARLY, init)
-    ref32 = _replay(root, init, 0, EARLY, bf16=False)
-    ref16 = _replay(root, init, 0, EARLY, bf16=True)
+    runs = _early_runs(tmp_path)
+    A, H, X, ref32, ref16 = runs["A"], runs["H"], runs["X"], runs["ref32"], runs["ref16"]
     d32 = np.abs(A - ref32)
     prefix = int(np.argmax(d32 > 0.01)) if (d32 > 0.01).any() else EARLY
     d16 = np.abs(H[:prefix] - ref16[:prefix])
@@ -144,40 +164,43 @@ def test_early_train_psnr_matches_reference_at_each_precision(tmp_path):
     for n, r in (("HIP fp32", A), ("fp32 replay", ref32), ("HIP bf16", H), ("bf16 replay", ref16), ("HIP bf16x3", X)):
         print(f"{n:12s}", np.round(r, 3).tolist())
     print(f"bf16 replayable prefix (within 0.05 dB of the bf16-operand replay): {p16} steps")
-    # bf16x3 in this regime (a re-created AdamW makes every step a sign step,
-    # so every near-zero gradient element whose sign a rounding-level change
-    # flips moves by the full lr): the reference's own reproducibility is the
-    # same replay computed by a second fp32 implementation (torch on the GPU
-    # instead of the CPU).  bf16x3 is held to (a) the north-star 0.05 dB of
-    # the fp32 replay over the first X3_FP32_STEPS steps (measured round 4:
-    # it first leaves at step 19) and (b) 0.05 dB of the replay of ITS OWN
-    # arithmetic (ref_cpu.OPS_BF16X3_K) over bf16x3's replayable prefix,
-    # >= X3_PREFIX steps -- the kernels compute what their emulation computes
-    # (as the bf16 case above).
-    from test_gpu_regime import chaos_horizon, first_exit
-    from test_gpu_train import _oracle_training
-    torch.manual_seed(1000)
-    np.random.seed(1000)
-    refg = np.array(_oracle_training(_hp(root, "fp32"), init, EARLY, 256, device="cuda")[0])
-    floor = np.abs(refg - ref32)
-    horizon = chaos_horizon(floor, EARLY)
-    dxr = np.abs(X - ref32)
-    refx3 = _replay(root, init, 0, EARLY, bf16=True, x3=True)
-    dxe = np.abs(X - refx3)
-    px3 = int(np.argmax(dxe > 0.05)) if (dxe > 0.05).any() else EARLY
-    print(f"reference on the GPU vs the CPU replay per step {np.round(floor, 4).tolist()}; horizon (within 0.025 dB) "
-          f"{horizon} of {EARLY} steps; first step past 0.05 dB: reference on the GPU {first_exit(floor)}, HIP fp32 "
-          f"{first_exit(d32)}, HIP bf16x3 {first_exit(dxr)}; HIP bf16x3 max |d| within the horizon "
-          f"{dxr[:horizon].max():.4f} dB")
-    print(f"bf16x3 replay {np.round(refx3, 3).tolist()}")
-    print(f"HIP bf16x3 vs its own replay per step {np.round(dxe, 4).tolist()}; replayable prefix (within 0.05 dB) "
-          f"{px3} of {EARLY} steps; emulation vs fp32 replay first past 0.05 dB: {first_exit(np.abs(refx3 - ref32))}")
+    print(f"HIP bf16x3f vs fp32 replay per step {np.round(np.abs(runs['XF'] - ref32), 4).tolist()}")
     assert prefix >= 20                       # fp32: the north-star 0.05 dB (0.01 here) over >= 20 steps
     assert p16 >= 5                           # bf16: within 0.05 dB of its own precision's replay
     assert d16[:p16].max() <= 0.05
-    assert dxr[:X3_FP32_STEPS].max() <= 0.05  # bf16x3 vs the fp32 replay
-    assert px3 >= X3_PREFIX                   # bf16x3 vs the replay of its own arithmetic
-    assert dxe[:px3].max() <= 0.05
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.xfail(strict=False, reason="bf16x3 leaves 0.05 dB of the fp32 replay at step 19 (0.09 dB) and of its "
+                   "own arithmetic's replay at step 17, inside the reference's own 29-step horizon (round 5, "
+                   "profiles/r05q/pytest_gpu.log): the north-star bar is not met in this sign-step regime")
+def test_early_bf16x3_over_the_reference_horizon(tmp_path):
+    """bf16x3 in the one-object regime, where a re-created AdamW makes every
+    step a sign step (every near-zero gradient element whose sign a
+    rounding-level change flips moves by the full lr).  The reference's own
+    reproducibility defines the window: the same replay computed by a second
+    fp32 implementation (torch on the GPU instead of the CPU) stays within
+    half the bar (0.025 dB) of the CPU replay for `horizon` steps.  Over that
+    horizon bf16x3 must stay within the north-star 0.05 dB of the fp32
+    replay, and within 0.05 dB of the replay of ITS OWN arithmetic
+    (ref_cpu.OPS_BF16X3_K: the kernels compute what their emulation
+    computes).  No step count here is taken from a bf16x3 measurement."""
+    from test_gpu_regime import chaos_horizon, first_exit
+    r = _early_runs(tmp_path)
+    X, ref32, refx3, refg = r["X"], r["ref32"], r["refx3"], r["refg"]
+    floor = np.abs(refg - ref32)
+    horizon = chaos_horizon(floor, EARLY)
+    dxr = np.abs(X - ref32)
+    dxe = np.abs(X - refx3)
+    print(f"\nreference on the GPU vs the CPU replay per step {np.round(floor, 4).tolist()}; horizon (within 0.025 dB) "
+          f"{horizon} of {EARLY} steps; first step past 0.05 dB: reference on the GPU {first_exit(floor)}, HIP fp32 "
+          f"{first_exit(np.abs(r['A'] - ref32))}, HIP bf16x3 {first_exit(dxr)}, HIP bf16x3 vs its own replay "
+          f"{first_exit(dxe)}, HIP bf16x3f {first_exit(np.abs(r['XF'] - ref32))}; HIP bf16x3 max |d| within the "
+          f"horizon {dxr[:horizon].max():.4f} dB (vs its own replay {dxe[:horizon].max():.4f})")
+    print(f"bf16x3 replay {np.round(refx3, 3).tolist()}")
+    assert horizon >= 10
+    assert dxr[:horizon].max() <= 0.05        # bf16x3 vs the fp32 replay
+    assert dxe[:horizon].max() <= 0.05        # bf16x3 vs the replay of its own arithmetic
 
 
 @pytest.mark.timeout(900)

@@ -12,10 +12,14 @@ identical initial weights and RNG draws through:
   * the HIP trainer in bf16x3 (error-compensated: weights AND chain
     operands carried as bf16 hi + lo pairs, three MFMAs per block --
     hi*hi + hi*lo + lo*hi -- into one fp32 accumulator),
+  * the HIP trainer in bf16x3f (the bf16x3 forward, the bf16 backward),
   * the fp32 CPU replay of the reference loop (oracle/ref_cpu.py),
 
 and asserts each one's per-step train PSNR (src/trainer.py:98-101) against the
-fp32 replay.
+fp32 replay over two epochs; over LONG_EPOCHS epochs and eight seeds against
+the reference replayed on the GPU (bf16x3 over the fp32 horizon per seed,
+seed 3 the recorded miss), and the converged state past the horizon (the
+seed-averaged tail mean) for bf16x3 and bf16x3f.
 """
 import numpy as np
 import pytest
@@ -80,7 +84,7 @@ def test_many_objects_train_psnr_vs_fp32_replay(tmp_path):
     root = _data(tmp_path)
     runs = {}
     runs["fp32"], init = _run(tmp_path, root, "fp32", REPLAY_STEPS)
-    for prec in ("bf16", "bf16x3"):
+    for prec in ("bf16", "bf16x3", "bf16x3f"):
         runs[prec], _ = _run(tmp_path, root, prec, REPLAY_STEPS, init)
     torch.set_num_threads(min(16, os.cpu_count() or 1))
     torch.manual_seed(1000)
@@ -100,7 +104,9 @@ def _epoch_means(r):
 
 FLOOR_DB = 0.025            # half the bar: the horizon ends where fp32 itself is half-way out
 BAR_DB = 0.05
-SEEDS = (0, 1, 2)
+SEEDS = tuple(range(8))
+SEED_X3_EXIT = 3            # the seed on which bf16x3 leaves the reference early (epoch 15 vs fp32's 33)
+TAIL_EPOCHS = 10            # converged-state criterion: the last TAIL_EPOCHS epoch means
 
 
 def chaos_horizon(floor, epochs=LONG_EPOCHS):
@@ -141,37 +147,91 @@ def horizon_report(label, seed, em, epochs):
     return horizon, gap
 
 
-@pytest.mark.timeout(900)
-def test_many_objects_long_horizon_vs_reference(tmp_path):
-    """LONG_EPOCHS epochs (the CPU replay would take hours) for three
-    initialisations: the HIP trainer in fp32 / bf16 / bf16x3 (and fp32 with
-    the dX / dW pass in one range, a second HIP summation order) against the
-    reference loop replayed in torch fp32 on the GPU, by epoch-mean train
-    PSNR.  Training in this regime is chaotic over hundreds of steps: the
-    trajectories of two fp32 implementations of the same loop separate by
-    tenths of a dB after 20-40 epochs (profiles/r04j_chaos.md: a second
-    torch summation order of the reference leaves 0.05 dB at epoch 28-32 or
-    not within 40, by seed).  The bar is therefore asserted over the
-    HORIZON where HIP fp32 itself stays within half of it (FLOOR_DB) of the
-    reference: there bf16x3 must stay within 0.05 dB of the reference.
-    bf16 is printed (it leaves 0.05 dB at epochs 12-21)."""
-    root = _data(tmp_path)
-    iters = LONG_EPOCHS * N_OBJ
-    bad = []
-    for seed in SEEDS:
+@pytest.fixture(scope="module")
+def regime_root(tmp_path_factory):
+    return _data(tmp_path_factory.mktemp("regime"))
+
+
+# epoch means of every run of a seed, shared by the per-seed horizon tests and
+# the converged-state test (each seed is trained once per session)
+_LONG = {}
+
+
+def long_runs(root, tmp_path, seed):
+    """LONG_EPOCHS epochs of the regime from one initialisation: HIP fp32,
+    HIP fp32 with the dX / dW pass in one range (a second HIP summation
+    order), bf16, bf16x3, bf16x3f, and the reference loop replayed in torch
+    fp32 on the GPU.  -> {run: epoch means}."""
+    if seed not in _LONG:
+        iters = LONG_EPOCHS * N_OBJ
         runs = {}
         runs["fp32"], init = _run(tmp_path, root, "fp32", iters, seed=seed)
         runs["fp32_order"], _ = _run(tmp_path, root, "fp32", iters, init, seed=seed, overlap=False)
-        for prec in ("bf16", "bf16x3"):
+        for prec in ("bf16", "bf16x3", "bf16x3f"):
             runs[prec], _ = _run(tmp_path, root, prec, iters, init, seed=seed)
         runs["ref"] = reference_on_gpu(root, init, iters, seed, hp_many(root, "fp32"))
-        em = {k: _epoch_means(v) for k, v in runs.items()}
-        horizon, gap = horizon_report("coarse", seed, em, LONG_EPOCHS)
-        assert em["ref"][-1] > em["ref"][0] + 3.0          # the run is learning
-        assert horizon >= 10                               # the floor leaves room for a meaningful window
-        if gap["bf16x3"][:horizon].max() > BAR_DB:
-            bad.append((seed, horizon, float(gap["bf16x3"][:horizon].max())))
-    assert not bad, bad
+        _LONG[seed] = ({k: _epoch_means(v) for k, v in runs.items()}, init)
+    return _LONG[seed]
+
+
+_X3_SEED3 = ("bf16x3 leaves 0.05 dB of the reference at epoch 15 on this seed, inside the fp32 horizon (32): "
+             "the known miss of the north-star PSNR bar (DESIGN.md section 4)")
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("seed", [pytest.param(s, marks=pytest.mark.xfail(reason=_X3_SEED3, strict=False))
+                                  if s == SEED_X3_EXIT else s for s in SEEDS])
+def test_long_horizon_vs_reference(regime_root, tmp_path, seed):
+    """LONG_EPOCHS epochs (the CPU replay would take hours) of the many-object
+    regime per initialisation: the HIP trainer in fp32 / bf16 / bf16x3 /
+    bf16x3f (and fp32 in a second HIP summation order) against the reference
+    loop replayed in torch fp32 on the GPU, by epoch-mean train PSNR.
+    Training in this regime is chaotic over hundreds of steps: the
+    trajectories of two fp32 implementations of the same loop separate by
+    tenths of a dB after 20-40 epochs (profiles/r04j_chaos.md).  The bar is
+    therefore asserted over the HORIZON where HIP fp32 itself stays within
+    half of it (FLOOR_DB) of the reference: there bf16x3 must stay within
+    0.05 dB of the reference, on every seed 0-7 (seed 3: expected to fail,
+    the recorded miss).  bf16 and bf16x3f (bf16 gradients) are printed; their
+    PSNR is asserted by test_converged_tail_psnr_vs_reference only."""
+    em, _ = long_runs(regime_root, tmp_path, seed)
+    horizon, gap = horizon_report("coarse", seed, em, LONG_EPOCHS)
+    assert em["ref"][-1] > em["ref"][0] + 3.0          # the run is learning
+    assert horizon >= 10                               # the floor leaves room for a meaningful window
+    assert gap["bf16x3"][:horizon].max() <= BAR_DB, (seed, horizon, float(gap["bf16x3"][:horizon].max()))
+
+
+@pytest.mark.timeout(1800)
+def test_converged_tail_psnr_vs_reference(regime_root, tmp_path):
+    """The converged state, past the chaos horizon: the mean train PSNR of
+    the last TAIL_EPOCHS epochs (of LONG_EPOCHS), averaged over the eight
+    initialisations, against the reference replayed on the GPU.  Past the
+    horizon two fp32 implementations of the reference differ by tenths of a
+    dB per seed, so the bar is the north-star 0.05 dB ON TOP of the
+    reference's own reproducibility: |mean_s(tail_prec - tail_ref)| <= 0.05 +
+    max(|mean_s(tail_fp32 - tail_ref)|, |mean_s(tail_fp32_order - tail_ref)|)
+    -- the seed-averaged differences of the two HIP fp32 summation orders,
+    printed beside it with the standard error over seeds.  Asserted for
+    bf16x3 and bf16x3f (the configurations whose rendered rgb meets the
+    1e-4 bar); bf16 printed."""
+    tails = {}
+    for seed in SEEDS:
+        em, _ = long_runs(regime_root, tmp_path, seed)
+        for k, v in em.items():
+            tails.setdefault(k, []).append(float(v[-TAIL_EPOCHS:].mean()))
+    t = {k: np.array(v) for k, v in tails.items()}
+    d = {k: t[k] - t["ref"] for k in t if k != "ref"}
+    se = {k: float(v.std(ddof=1) / np.sqrt(len(v))) for k, v in d.items()}
+    floor = max(abs(float(d["fp32"].mean())), abs(float(d["fp32_order"].mean())))
+    bar = BAR_DB + floor
+    print(f"\nconverged tail (last {TAIL_EPOCHS} of {LONG_EPOCHS} epochs), reference per seed "
+          f"{np.round(t['ref'], 3).tolist()}")
+    for k, v in d.items():
+        print(f"tail {k:10s} - reference per seed {np.round(v, 3).tolist()}: mean {v.mean():+.4f} dB "
+              f"(standard error {se[k]:.4f})")
+    print(f"reference reproducibility (two HIP fp32 orders): {floor:.4f} dB; bar 0.05 + that = {bar:.4f} dB")
+    assert abs(float(d["bf16x3"].mean())) <= bar, (float(d["bf16x3"].mean()), bar)
+    assert abs(float(d["bf16x3f"].mean())) <= bar, (float(d["bf16x3f"].mean()), bar)
 
 
 @pytest.mark.timeout(600)
@@ -193,7 +253,7 @@ def test_render_psnr_same_weights_across_precisions(tmp_path):
     ds = SRN("srn_cars", "cars_train", root, 2, crop_img=False, n_train_views=2)
     z = torch.linspace(0.8 + 0.5 / N, 1.8 - 0.5 / N, N, device="cuda")
     psnr = {}
-    for prec in ("fp32", "bf16", "bf16x3", "fp32"):
+    for prec in ("fp32", "bf16", "bf16x3", "bf16x3f", "fp32"):
         m = CodeNeRF(3, 1, precision=prec)
         m.load_state_dict(sd)
         m = m.cuda()
@@ -223,17 +283,16 @@ def test_render_psnr_same_weights_across_precisions(tmp_path):
           f"max |bf16 - fp32| {d16:.5f} dB, max |bf16x3 - fp32| {dx3:.6f} dB")
     assert psnr["fp32"].mean() > tr_psnr[:N_OBJ].mean()      # trained past init
     assert dx3 <= 1e-3
+    assert np.array_equal(psnr["bf16x3f"], psnr["bf16x3"])    # the same forward chains
     assert d16 <= 0.05
 
 
-SEED_X3_EXIT = 3            # the seed on which bf16x3 leaves the reference early (round 4: epoch 15 vs fp32's 33)
-
-
 @pytest.mark.timeout(900)
-def test_seed3_bf16x3_exit_is_its_arithmetic(tmp_path):
-    """Seed 3, where HIP bf16x3 leaves 0.05 dB of the reference at epoch 15
-    while HIP fp32 holds to 33: the exit belongs to the bf16x3 ARITHMETIC, not
-    to a kernel defect.  The same loop replayed in torch on the GPU with the
+def test_seed3_diagnostic_exit_follows_the_x3_arithmetic(regime_root, tmp_path):
+    """DIAGNOSTIC, not parity evidence (the parity miss itself is the xfail
+    of test_long_horizon_vs_reference[3]).  Seed 3, where HIP bf16x3 leaves
+    0.05 dB of the reference at epoch 15 while HIP fp32 holds to 33: the exit
+    belongs to the bf16x3 ARITHMETIC, not to a kernel defect.  The same loop replayed in torch on the GPU with the
     kernels' arithmetic op for op (ref_cpu.OPS_BF16X3_K: hi + lo operands in
     three products, the dW X split, the latent path from the bf16 dA sums,
     the encoding_shape fold -- tests/test_gpu_x3_trace.py shows the kernels
@@ -245,19 +304,16 @@ def test_seed3_bf16x3_exit_is_its_arithmetic(tmp_path):
     first is chaos)"""
     from oracle import ref_cpu
     from test_gpu_train import _oracle_training
-    root = _data(tmp_path)
+    root = regime_root
     seed = SEED_X3_EXIT
     iters = LONG_EPOCHS * N_OBJ
-    runs = {}
-    runs["fp32"], init = _run(tmp_path, root, "fp32", iters, seed=seed)
-    runs["bf16x3"], _ = _run(tmp_path, root, "bf16x3", iters, init, seed=seed)
-    runs["ref"] = reference_on_gpu(root, init, iters, seed, hp_many(root, "fp32"))
+    em_all, init = long_runs(root, tmp_path, seed)
+    em = {k: em_all[k] for k in ("fp32", "bf16x3", "ref")}
     torch.manual_seed(1000 + seed)
     np.random.seed(1000 + seed)
     with ref_cpu.bf16_operands(ops=ref_cpu.OPS_BF16X3_K, layer_ops=ref_cpu.X3_LAYER_OPS):
         ps, _, _, _ = _oracle_training(hp_many(root, "fp32"), init, iters, B, device="cuda")
-    runs["x3_emulation"] = np.array(ps)
-    em = {k: _epoch_means(v) for k, v in runs.items()}
+    em["x3_emulation"] = _epoch_means(np.array(ps))
     horizon, gap = horizon_report("coarse", seed, em, LONG_EPOCHS)
     e_hip, e_emu = first_exit(gap["bf16x3"]), first_exit(gap["x3_emulation"])
     print(f"seed {seed}: first epoch past {BAR_DB} dB -- HIP bf16x3 {e_hip}, its emulation {e_emu}, horizon {horizon}")

@@ -24,16 +24,22 @@ N_SIMD = 1024      # 256 CUs x 4
 N_XCD = 8
 
 
+# chain-kernel precision template argument of the forward / backward chains
+# of each plan (bf16x3f: the bf16x3 forward, the bf16 backward)
+FWD_P = {"fp32": 0, "bf16": 1, "bf16x3": 2, "bf16x3f": 2}
+BWD_P = {"fp32": 0, "bf16": 1, "bf16x3": 2, "bf16x3f": 1}
+
+
 def short(name, prec):
     m = re.search(r"chain(?:16)?_kernel<(\d), \d, \d, (true|false), \d+, (\d)>", name)
-    if m and int(m.group(1)) != prec:
-        return None
     if m:
-        mode = int(m.group(3))
         kind = "bwd" if m.group(2) == "true" else "fwd"
-        return kind if mode == 1 else f"{kind}_codes" if mode == 2 else f"{kind}_infer"
+        if int(m.group(1)) != (BWD_P if kind == "bwd" else FWD_P)[prec]:
+            return None
+        mode = int(m.group(3))       # 1 train, 3 train (hi planes only), 2 codes, 0 infer
+        return kind if mode in (1, 3) else f"{kind}_codes" if mode == 2 else f"{kind}_infer"
     m = re.search(r"\bdw_kernel<(\d)>", name)
-    if m and int(m.group(1)) == min(prec, 1):     # bf16x3 stores bf16 planes: the bf16 dW pass
+    if m and int(m.group(1)) == min(FWD_P[prec], 1):     # every bf16 plan stores bf16 planes: the bf16 dW pass
         return "dw"
     return None
 
@@ -57,7 +63,6 @@ def main():
     src, tag = sys.argv[1:3]
     config = sys.argv[3] if len(sys.argv) > 3 else "c2"
     precision = sys.argv[4] if len(sys.argv) > 4 else ("fp32" if config == "c5" else "bf16")
-    pcode = {"fp32": 0, "bf16": 1, "bf16x3": 2}[precision]
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     prof = os.path.join(repo, "profiles")
     os.makedirs(prof, exist_ok=True)
@@ -94,7 +99,7 @@ def main():
         lines.append(f"| `{name[:90]}` | {r['Calls']} | {avg_ns / 1e3:.1f} | {float(r['Percentage']):.2f} | "
                      f"{fmt(hbm and hbm / 1e9, 3)} | {fmt(gbs, 1)} | {fmt(tfl, 4)} | {fmt(pmc_ns and pmc_ns / 1e3, 1)} | "
                      f"{fmt(util, 3)} | {fmt(clk, 2)} |")
-        s = short(name, pcode)
+        s = short(name, precision)
         if s and hbm:
             traffic[s] = {"hbm_bytes": int(hbm), "fetch_kib": f, "write_kib": w, "avg_ns": avg_ns,
                           "mfma_util": util, "eff_clock_ghz": clk, "pmc_pass_avg_ns": pmc_ns, "mfma_flop": mops * 512 if mops else None,
