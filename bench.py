@@ -3,7 +3,11 @@
 Workload (BASELINE.json configs[1]): srncar.json network (3 shape blocks,
 1 texture block, W = 256), one 128x128 image per object per step, 64 coarse
 + 64 fine samples per ray (128 MLP evaluations per ray), bf16 MFMA with fp32
-accumulation, synthetic SRN-cars-like data (targets ray-cast from an
+accumulation -- by default the bf16x3f plan: the forward chains carry every
+weight and activation as a bf16 hi + lo pair (three bf16 MFMAs per block:
+rendered rgb within 1e-4 of the fp32 reference, the north-star bar), the
+backward runs on bf16 operands; bf16, bf16x3 and fp32 are measured in the same
+line (``precisions``) -- synthetic SRN-cars-like data (targets ray-cast from an
 ellipsoid object by the SRN-format generator's renderer, cameras on a
 radius-1.3 sphere, focal 131.25, near/far 0.8/1.8; no dataset is available
 offline; --config c3 uses the srnchair.json geometry: near/far 1.25/2.75,
@@ -45,6 +49,19 @@ DW_FOLD_FLOP = 2 * 2 * 257 ** 3
 DW_BYTES_PER_SAMPLE = {"bf16": 6_976, "bf16x3": 10_432, "bf16x3f": 6_976,
                        "fp32": 13_952}   # + the X lo planes in bf16x3; bf16x3f's dW is the bf16 one
 PRECISIONS = ("bf16", "bf16x3", "bf16x3f", "fp32")
+PRECISION_NOTE = {
+    "bf16": "bf16 operands everywhere (rendered rgb ~2e-4 from the fp32 reference)",
+    "bf16x3": "forward and dX chains on bf16 hi + lo operands and weights (3 MFMAs per block), dW on hi + lo X "
+              "operands: fp32-class rgb and gradients",
+    "bf16x3f": "the bf16x3 forward chains (fp32-class rendered rgb) + the bf16 backward (dX chain and dW on bf16 "
+               "operands)",
+    "fp32": "exact fp32 MFMA (v_mfma_f32_32x32x2_f32)",
+}
+
+
+def dtype_of(precision):
+    """the arithmetic type the path computes in: MFMA operand type"""
+    return "fp32" if precision == "fp32" else "bf16"
 KERNEL_NAMES = {"fwd": "chain_kernel<fwd,train>", "bwd": "chain_kernel<bwd>", "dw": "dw_kernel"}
 # SURVEY.md 8(d): algorithmic HBM bytes per ray of the fused ray-major step
 # (24 B origin + direction in, 12 B gt, 12 B rgb out)
@@ -64,7 +81,7 @@ def parse():
     ap.add_argument("--H", type=int, default=128)
     ap.add_argument("--n-coarse", type=int, default=64)
     ap.add_argument("--n-fine", type=int, default=64)
-    ap.add_argument("--precision", default="bf16", choices=list(PRECISIONS),
+    ap.add_argument("--precision", default="bf16x3f", choices=list(PRECISIONS),
                     help="chain arithmetic: bf16 operands | bf16x3 (hi + lo operands, 3 MFMAs per block) | "
                          "bf16x3f (the bf16x3 forward, the bf16 backward) | fp32")
     ap.add_argument("--objects", type=int, default=64)
@@ -394,7 +411,8 @@ def main():
             ms2 = dt2 / n2 * 1e3
             others[prec] = {"value": round(samples_per_step * world * n2 / dt2, 1), "unit": "ray-samples/s",
                             "ms_per_step": round(ms2, 3), "ms_per_step_median": round(med2, 3),
-                            "steps": n2, "dtype": prec,
+                            "steps": n2, "dtype": dtype_of(prec), "precision": prec,
+                            "precision_note": PRECISION_NOTE[prec],
                             "roofline": roofline(args, t2, samples_per_step, ms2,
                                                  wl2["core"].step_impl.overlap_dw, precision=prec, steps=n2)}
             del wl2
@@ -415,7 +433,7 @@ def main():
             "value": round(value, 1), "unit": "ray-samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "ms_per_step_median": round(median, 3),
             "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
+            "scaling": "weak", "vs_baseline": None, "dtype": dtype_of(args.precision),
             "data": f"synthetic ({H}x{H} ray-cast ellipsoid object per rank, poses on a radius-{radius} sphere, "
                     + (f"trained weights {os.path.relpath(weights_path(args), REPO)})" if weights_path(args)
                        else "random-init weights)"),
@@ -423,7 +441,8 @@ def main():
                                    f"samples/ray, " + {"c4": "50 views, codes-only fwd+dX+AdamW",
                                                        "c4eval": "one held-out view per step, forward-only + MSE"}.get(
                                        args.config, "train step incl. AdamW"),
-                       "name": args.config, "objects_per_step": world,
+                       "name": args.config, "precision": args.precision,
+                       "precision_note": PRECISION_NOTE[args.precision], "objects_per_step": world,
                        "rays_per_step_per_gpu": R, "parallelism": f"dp{world}"},
             "roofline": roof,
             "clock": dict(clock, note=CLOCK_NOTE),
@@ -437,28 +456,31 @@ def main():
 
 CLOCK_NOTE = ("effective shader clock of this box under a dense bf16 MFMA load (cn_clock_probe: every CU, "
               "back-to-back v_mfma_f32_32x32x16_bf16 on hashed operands, s_memtime / s_memrealtime stamps, median "
-              "over workgroups), measured before the warm-up and after the timed steps: step times of two runs "
-              "compare at these clocks")
+              "over workgroups; the last of 8 back-to-back ~3 ms launches), measured before the warm-up, after "
+              "the timed steps and after the secondary precisions: step times of two runs compare at these clocks")
 
 
-def clock_probe(dev, n_wg=1024, iters=12000):
-    """cn_clock_probe on ``dev``: {"ghz", "bf16_tflops", "ms"} -- the median
-    over workgroups of stamped shader cycles / 100 MHz ticks, and the probe's
-    own MFMA rate (n_wg x 4 waves x iters x 4 MFMAs x 32,768 FLOP / wall)."""
+def clock_probe(dev, n_wg=1024, iters=12000, reps=8):
+    """cn_clock_probe on ``dev``, ``reps`` launches back to back (~3 ms each,
+    so the clock settles under the load): {"ghz", "ghz_first", "bf16_tflops",
+    "ms"} -- the last launch's median over workgroups of stamped shader cycles
+    / 100 MHz ticks (and the first launch's), its MFMA rate (n_wg x 4 waves x
+    iters x 4 MFMAs x 32,768 FLOP / its wall time) and that wall time."""
     import numpy as np
     from codenerf_amd import _lib
     L = _lib.lib()
-    out = torch.zeros(3 * n_wg, dtype=torch.int32, device=dev)
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record()
-    _lib.check(L.cn_clock_probe(_lib.ptr(out), n_wg, iters, 12345, _lib.stream_ptr(dev)), "cn_clock_probe")
-    b.record()
+    out = torch.zeros(reps, 3 * n_wg, dtype=torch.int32, device=dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
+    ev[0].record()
+    for r in range(reps):
+        _lib.check(L.cn_clock_probe(_lib.ptr(out[r]), n_wg, iters, 12345 + r, _lib.stream_ptr(dev)), "cn_clock_probe")
+        ev[r + 1].record()
     torch.cuda.synchronize(dev)
-    o = out.cpu().numpy().view(np.uint32).reshape(-1, 3).astype(np.float64)
-    ghz = float(np.median(o[:, 0] / np.maximum(o[:, 1], 1))) * 0.1
-    ms = a.elapsed_time(b)
+    o = out.cpu().numpy().view(np.uint32).reshape(reps, -1, 3).astype(np.float64)
+    ghz = [float(np.median(o[r, :, 0] / np.maximum(o[r, :, 1], 1))) * 0.1 for r in range(reps)]
+    ms = ev[reps - 1].elapsed_time(ev[reps])
     tf = n_wg * 4 * iters * 4 * 32768 / (ms * 1e-3) / 1e12
-    return {"ghz": round(ghz, 4), "bf16_tflops": round(tf, 1), "ms": round(ms, 3)}
+    return {"ghz": round(ghz[-1], 4), "ghz_first": round(ghz[0], 4), "bf16_tflops": round(tf, 1), "ms": round(ms, 3)}
 
 
 def kernel_roofline(k, precision, timers, traffic):

@@ -6,7 +6,7 @@
 export TMPDIR=/tmp
 OUT=gpurun_out/r06b
 mkdir -p $OUT
-timeout -k 10 1150 python -u -m pytest -v -rxX --timeout 1100 --timeout-method thread tests/test_gpu_regime.py \
+timeout -k 10 1150 python -u -m pytest -v -rA --timeout 1100 --timeout-method thread tests/test_gpu_regime.py \
   > $OUT/pytest_regime.log 2>&1
 rc=$?
 echo "pytest rc=$rc"

@@ -4,7 +4,7 @@
 export TMPDIR=/tmp
 OUT=gpurun_out/r06c
 mkdir -p $OUT
-timeout -k 10 1150 python -u -m pytest -v -rxX --timeout 1100 --timeout-method thread tests/test_gpu_regime_fine.py \
+timeout -k 10 1150 python -u -m pytest -v -rA --timeout 1100 --timeout-method thread tests/test_gpu_regime_fine.py \
   tests/test_gpu_converge.py > $OUT/pytest_fine_converge.log 2>&1
 rc=$?
 echo "pytest rc=$rc"
