@@ -125,6 +125,20 @@ CN_DEV void plane_store(__amdgpu_buffer_rsrc_t r, const uint32_t* voff, int t, i
                         float a, float b, float c, float d) {
   bstore4<E>(r, voff[g], t * (1024 * (int)sizeof(E)), a, b, c, d);
 }
+// groups 2gp and 2gp + 1 of feature tile t (8 consecutive values of a lane
+// half's slots): bf16 one 16-B store (the pair-block layout puts the two
+// quads side by side), fp32 two 16-B stores
+template <class E>
+CN_DEV void plane_store_oct(__amdgpu_buffer_rsrc_t r, const uint32_t* voff, int t, int gp, const float* v) {
+  if constexpr (sizeof(E) == 2) {
+    bstore128(r, voff[2 * gp],
+              u32x4{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7])},
+              t * 2048);
+  } else {
+    plane_store<E>(r, voff, t, 2 * gp, v[0], v[1], v[2], v[3]);
+    plane_store<E>(r, voff, t, 2 * gp + 1, v[4], v[5], v[6], v[7]);
+  }
+}
 // Buffer descriptor of wave wglob's 32-sample slab of a plane of width F: the
 // 64-bit slab base is wave-uniform (scalar arithmetic) and goes into the
 // descriptor, so every per-store offset stays below one slab (<= 36 KiB).  No
@@ -134,17 +148,15 @@ CN_DEV __amdgpu_buffer_rsrc_t slab_rsrc(const void* plane, int F, int wglob, boo
   return mkrsrc((const char*)plane + (size_t)wglob * (size_t)F * 32u * sizeof(E), live);
 }
 // bf16: groups 2gp and 2gp+1 of feature tile t (this lane: features 16gp +
-// 4h .. +3 in a, 16gp + 8 + 4h .. +3 in b, as packed pairs) -> two 8-B stores
-// at their places in the bf16 pair-block layout (cn_layout.h: voff[2gp] /
-// voff[2gp + 1] = slab_off of those features).  Each store instruction still
-// writes one contiguous 512 B (32 positions x 16 B, both lane halves), and
-// the operand registers are stored as they are: no lane exchange, so no
-// register copies, and none of the wait states a store fed by
-// v_permlane32_swap needed on gfx950 (its first data dword was read after
-// the next VALU had rewritten it -- round 3's 16-B store path).
+// 4h .. +3 in a, 16gp + 8 + 4h .. +3 in b, as packed pairs) -> ONE 16-B store
+// at voffa = slab_off(s, 16gp + 4h): the pair-block layout (cn_layout.h) puts
+// exactly these two quads side by side, so the operand registers are stored
+// as they are (no lane exchange, no register copies) and one store
+// instruction writes the whole 1 KiB pair block (rounds 4-5: two 8-B
+// stores of 512 B each; voffb = voffa + 8 is implied).
 CN_DEV void plane_store_pair(__amdgpu_buffer_rsrc_t r, uint32_t voffa, uint32_t voffb, int t, u32x2 a, u32x2 b) {
-  bstore64(r, voffa, a, t * 2048);
-  bstore64(r, voffb, b, t * 2048);
+  (void)voffb;
+  bstore128(r, voffa, u32x4{a[0], a[1], b[0], b[1]}, t * 2048);
 }
 
 template <int P, int SB, int TB, bool BWD, int WAVES, int MODE>
@@ -228,6 +240,15 @@ struct Chain {
   static constexpr int kSbMask = 0x6;
   static constexpr int kRingBytes = NS * kChunkBytes;
   static constexpr int kBlobFloats = BiasBlob<SB, TB>::kFloats;
+  static constexpr int kBlobIters = (kBlobFloats / 4 + WAVES * 64 - 1) / (WAVES * 64);
+  // the first D weight chunks are issued before the prologue (run())
+  static constexpr bool kEarlyIssue = true;
+  // VMEM stores of the prologue (forward: PE, dir and, bf16x3 training, PE
+  // lo planes; backward: the drgb plane and the sigma-head columns), as
+  // plane_store_oct instructions: issued after the early weight chunks, so
+  // younger than them at their wait points
+  static constexpr int kProStores =
+      !PLANES ? 0 : !BWD ? (kBf16 ? 4 + 2 + (kXlo ? 4 : 0) : 8 + 4) : (kBf16 ? 4 : 8);
   static constexpr int kWsOff = BiasBlob<SB, TB>::kWs;
   static constexpr int kMiscOff = BiasBlob<SB, TB>::kMisc;
   static constexpr int kDirStash = (kBf16 && !kX3) ? 32 : 64;      // bytes per lane (bf16x3: hi, lo)
@@ -267,17 +288,20 @@ struct Chain {
   }
 
   // ---------------- compile-time vmcnt bookkeeping
+  // plane store instructions per 32-feature tile: bf16 one 16-B store per
+  // pair block (plane_store_pair), fp32 one 16-B store per 4-feature group
+  static constexpr int kStoresPerTile = kBf16 ? 2 : 4;
   // Vector-memory instructions each wave issues in a layer epilogue.
   static constexpr int stores_of_layer(int i) {
     const Layer l = S::L(i);
     if (!BWD) {
       int s = 0;
-      if (plane_of(i) && !defers(i)) s += l.T * 4;     // 4 stores per tile (bf16: 2 pairs x 2)
+      if (plane_of(i) && !defers(i)) s += l.T * kStoresPerTile;
       if (TRAIN && l.mask >= 0) s += 1;
       if (l.epi == EPI_SHAPE) s += TRAIN ? 2 : 1;
       return s;   // EPI_RGB stores come after the last wait: not counted (safe)
     }
-    return plane_of(i) && !defers(i) ? l.T * 4 : 0;
+    return plane_of(i) && !defers(i) ? l.T * kStoresPerTile : 0;
   }
   // ---------------- epilogue schedule (see the epilogues below)
   // layers whose epilogue is spread over the next layer's first tile
@@ -322,7 +346,7 @@ struct Chain {
       if (!diag(i) && S::last_block(i) == g) s += stores_of_layer(i);
       if (diag(i) && final_block(i) == g) s += final_stores(i);
     }
-    if (deferred_at(g) >= 0) s += kXlo ? 4 : 2;     // one (or, with the lo plane, two) pair stores
+    if (deferred_at(g) >= 0) s += kXlo ? 2 : 1;     // one (or, with the lo plane, two) 16-B pair stores
     return s;
   }
   static constexpr int stores_between(int b0, int b1) {
@@ -351,6 +375,7 @@ struct Chain {
     int n = 0;
     if (c < D) {
       for (int i = c + 1; i < D; ++i) n += issued(i);        // the initial issue, younger than c
+      n += kProStores;                                       // the prologue's plane stores after it
       for (int w = 0; w < c; ++w) n += issued(w + D);        // wait points 0 .. c-1
       n += stores_between(0, wp(c));
     } else {
@@ -376,9 +401,32 @@ struct Chain {
 #pragma unroll
     for (int g = 0; g < 4; ++g) voff[g] = (uint32_t)slab_off(lane & 31, 8 * g + 4 * h, (int)sizeof(E));
 
-    // -- per-call bias blob -> LDS (plain loads; nothing is in flight yet)
-    for (int i = threadIdx.x; i < kBlobFloats / 4; i += WAVES * 64)
-      ((f32x4*)prm)[i] = ((const f32x4*)a.bias)[i];
+    // -- per-call bias blob (-> LDS below) and, forward, the sample inputs:
+    // plain loads issued before the weight stream, so waiting for them does
+    // not wait for its LDS-DMA (vmcnt counts in issue order)
+    f32x4 blobv[kBlobIters];
+#pragma unroll
+    for (int j = 0; j < kBlobIters; ++j) {
+      const int i = threadIdx.x + j * WAVES * 64;
+      if (i < kBlobFloats / 4) blobv[j] = ((const f32x4*)a.bias)[i];
+    }
+    Inputs in{};
+    BwdInputs bwd_in{};
+    if constexpr (!BWD) in = load_inputs(a, mc);
+    else bwd_in = load_bwd_inputs(a, m, mc, wglob, lane);
+    // forward: the first D chunks of the weight stream are issued now and land
+    // during the prologue (the positional encoding: 22 accurate sincosf per
+    // lane in bf16x3), instead of after it
+    if constexpr (kEarlyIssue) {
+      __builtin_amdgcn_sched_barrier(0);
+      static_for<0, D>([&](auto i) { issue<i>(a, smem, w, lane); });
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int j = 0; j < kBlobIters; ++j) {
+      const int i = threadIdx.x + j * WAVES * 64;
+      if (i < kBlobFloats / 4) ((f32x4*)prm)[i] = blobv[j];
+    }
 
     BinT bin[kBin];
     BinT binl[kX3 ? kBin : 1];     // bf16x3: the operand's lo parts
@@ -395,14 +443,14 @@ struct Chain {
 
     float ds = 0.f;   // bwd: sigma-head pre-activation gradient of this sample
     if constexpr (!BWD) {
-      prologue_fwd(a, bin, binl, smem, h, lane, w, m, mc, wglob, voff);
+      prologue_fwd(a, bin, binl, smem, h, lane, w, m, mc, wglob, voff, in);
     } else {
-      ds = prologue_bwd(a, bin, binl, smem, h, lane, w, m, mc, wglob, voff);
+      ds = prologue_bwd(a, bin, binl, smem, h, lane, w, wglob, voff, bwd_in);
     }
     __syncthreads();
     if constexpr (!BWD) load_bias<0>(acc, prm, h);
 
-    static_for<0, D>([&](auto i) { issue<i>(a, smem, w, lane); });
+    if constexpr (!kEarlyIssue) static_for<0, D>([&](auto i) { issue<i>(a, smem, w, lane); });
 
     float sig_part = 0.f;
     MaskAcc mk;
@@ -566,20 +614,31 @@ struct Chain {
   }
 
   // ---------------- prologues
-  __device__ static void prologue_fwd(const ChainArgs& a, BinT* bin, BinT* binl, char* smem, int h, int lane,
-                                      int w, int m, int mc, int wglob, const uint32_t* voff) {
-    float x[3], d[3];
+  // The forward's per-sample inputs, loaded before the weight stream is
+  // issued (run()): explicit points, or ray origin / direction and z
+  struct Inputs {
+    float o[3], d[3], z;
+  };
+  __device__ static Inputs load_inputs(const ChainArgs& a, int mc) {
+    Inputs in;
     if (a.mode == 0) {
-      for (int k = 0; k < 3; ++k) { x[k] = a.xyz[3 * mc + k]; d[k] = a.vdir[3 * mc + k]; }
+      for (int k = 0; k < 3; ++k) { in.o[k] = a.xyz[3 * mc + k]; in.d[k] = a.vdir[3 * mc + k]; }
+      in.z = 0.f;
     } else {
       const int r = mc / a.nsamp;
       const int s = mc - r * a.nsamp;
-      const float z = a.zvals[r * a.z_stride + s];
-      for (int k = 0; k < 3; ++k) {
-        d[k] = a.rays_d[3 * r + k];
-        // xyz = ro + vd * z  (src/utils.py:30), no fused multiply-add
-        x[k] = fadd_rn(a.rays_o[3 * r + k], fmul_rn(d[k], z));
-      }
+      in.z = a.zvals[r * a.z_stride + s];
+      for (int k = 0; k < 3; ++k) { in.o[k] = a.rays_o[3 * r + k]; in.d[k] = a.rays_d[3 * r + k]; }
+    }
+    return in;
+  }
+  __device__ static void prologue_fwd(const ChainArgs& a, BinT* bin, BinT* binl, char* smem, int h, int lane,
+                                      int w, int m, int mc, int wglob, const uint32_t* voff, const Inputs& in) {
+    float x[3], d[3];
+    for (int k = 0; k < 3; ++k) {
+      d[k] = in.d[k];
+      // xyz = ro + vd * z  (src/utils.py:30), no fused multiply-add
+      x[k] = a.mode == 0 ? in.o[k] : fadd_rn(in.o[k], fmul_rn(in.d[k], in.z));
     }
     // positional encodings: this lane half's 32 PE slots and 16 dir slots
     float pe[32], dp[16];
@@ -641,42 +700,57 @@ struct Chain {
     }
     if constexpr (PLANES) {
       // slot q of lane half h -> column slot_col(h, q): group k = q / 4 lands in
-      // feature tile k / 4, group k % 4 (cn_layout.h)
+      // feature tile k / 4, group k % 4 (cn_layout.h); groups 2gp, 2gp + 1 of
+      // a tile as one plane_store_oct (bf16: one 16-B store) -- explicit, so
+      // kProStores counts exactly the store instructions issued here
       const auto rp = slab_rsrc<E>(a.pe, 64, wglob);
 #pragma unroll
-      for (int k = 0; k < 8; ++k)
-        plane_store<E>(rp, voff, k >> 2, k & 3, pe[4 * k], pe[4 * k + 1], pe[4 * k + 2], pe[4 * k + 3]);
+      for (int j = 0; j < 4; ++j) plane_store_oct<E>(rp, voff, j >> 1, j & 1, pe + 8 * j);
       const auto rd = slab_rsrc<E>(a.dir, 32, wglob);
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        plane_store<E>(rd, voff, 0, k, dp[4 * k], dp[4 * k + 1], dp[4 * k + 2], dp[4 * k + 3]);
+      for (int j = 0; j < 2; ++j) plane_store_oct<E>(rd, voff, 0, j, dp + 8 * j);
       if constexpr (kXlo) {
         // the PE operand's lo parts (the dir-PE tile of encoding_viewdir's
         // dW stays hi only: its staged slab would not fit the LDS ring)
-        auto lo = [](float x) { return x - (float)(__bf16)x; };
+        float pl[32];
+#pragma unroll
+        for (int q = 0; q < 32; ++q) pl[q] = pe[q] - (float)(__bf16)pe[q];
         const auto rpl = slab_rsrc<E>(a.pelo, 64, wglob);
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-          plane_store<E>(rpl, voff, k >> 2, k & 3, lo(pe[4 * k]), lo(pe[4 * k + 1]), lo(pe[4 * k + 2]),
-                         lo(pe[4 * k + 3]));
+        for (int j = 0; j < 4; ++j) plane_store_oct<E>(rpl, voff, j >> 1, j & 1, pl + 8 * j);
       }
     }
   }
 
-  __device__ static float prologue_bwd(const ChainArgs& a, BinT* bin, BinT* binl, char* smem, int h, int lane,
-                                       int w, int m, int mc, int wglob, const uint32_t* voff, bool live = true,
-                                       int wread = -1) {
-    if (wread < 0) wread = wglob;       // slab the masks are read from (clamped for a dead wave)
+  // The backward's per-sample inputs (upstream gradients, sigma-head
+  // pre-activation, the wave's ReLU mask words), loaded before the weight
+  // stream is issued (run())
+  struct BwdInputs {
+    float g0, g1, g2, dsig, spre;
+    u32x4 mw[N::kMasks];
+  };
+  __device__ static BwdInputs load_bwd_inputs(const ChainArgs& a, int m, int mc, int wglob, int lane) {
+    BwdInputs in;
     // padding samples (m >= M) get zero upstream gradients, so every dA they
     // write is exactly 0 and the dW pass can sum whole 32-sample tiles
     const bool valid = m < a.M;
-    const float g0 = valid ? a.drgb[3 * mc + 0] : 0.f;
-    const float g1 = valid ? a.drgb[3 * mc + 1] : 0.f;
-    const float g2 = valid ? a.drgb[3 * mc + 2] : 0.f;
+    in.g0 = valid ? a.drgb[3 * mc + 0] : 0.f;
+    in.g1 = valid ? a.drgb[3 * mc + 1] : 0.f;
+    in.g2 = valid ? a.drgb[3 * mc + 2] : 0.f;
+    in.dsig = valid ? a.dsigma[mc] : 0.f;
+    in.spre = a.spre[mc];
+    const u32x4* src = (const u32x4*)a.masks + (size_t)wglob * N::kMasks * 64 + lane;
+#pragma unroll
+    for (int k = 0; k < N::kMasks; ++k) in.mw[k] = src[k * 64];
+    return in;
+  }
+  __device__ static float prologue_bwd(const ChainArgs& a, BinT* bin, BinT* binl, char* smem, int h, int lane,
+                                       int w, int wglob, const uint32_t* voff, const BwdInputs& in) {
+    const float g0 = in.g0, g1 = in.g1, g2 = in.g2;
     // Softplus backward exactly as torch: grad * (x > 20 ? 1 : e^x / (e^x + 1))
-    const float s = a.spre[mc];
+    const float s = in.spre;
     const float ex = expf(s);
-    const float ds = valid ? a.dsigma[mc] * (s > 20.f ? 1.f : ex / (ex + 1.f)) : 0.f;
+    const float ds = in.dsig * (s > 20.f ? 1.f : ex / (ex + 1.f));
     if constexpr (kBf16) {
       // k-step 0, lane half h, element j -> drgb component 8h + j
       if (h == 0) {
@@ -690,25 +764,25 @@ struct Chain {
     }
     if constexpr (PLANES) {
       // drgb as a padded 32-wide plane for the rgb-head weight gradient
-      // (columns slot_col(0, 0..2) = 0..2)
-      const auto r8 = slab_rsrc<E>(a.d8, 32, wglob, live);
-      plane_store<E>(r8, voff, 0, 0, h ? 0.f : g0, h ? 0.f : g1, h ? 0.f : g2, 0.f);
-#pragma unroll
-      for (int k = 1; k < 4; ++k) plane_store<E>(r8, voff, 0, k, 0.f, 0.f, 0.f, 0.f);
-      // the sigma-head gradient rides in columns 256 (value) and 257 (its
-      // rounding residual, so bf16 storage keeps ~16 significant bits) of the
-      // viewdir dA plane (feature tile 8 of its 288 columns)
-      const auto rv = slab_rsrc<E>(a.dA[SB + 2], 288, wglob, live);
+      // (columns slot_col(0, 0..2) = 0..2); the sigma-head gradient rides in
+      // columns 256 (value) and 257 (its rounding residual, so bf16 storage
+      // keeps ~16 significant bits) of the viewdir dA plane (feature tile 8 of
+      // its 288 columns).  Explicit 16-B stores: kProStores counts them.
       const float ds_hi = (float)(E)ds;
-      plane_store<E>(rv, voff, 8, 0, h ? 0.f : ds_hi, h ? 0.f : ds - ds_hi, 0.f, 0.f);
-#pragma unroll
-      for (int k = 1; k < 4; ++k) plane_store<E>(rv, voff, 8, k, 0.f, 0.f, 0.f, 0.f);
+      const float z8[8] = {};
+      const float d8v[8] = {h ? 0.f : g0, h ? 0.f : g1, h ? 0.f : g2, 0.f, 0.f, 0.f, 0.f, 0.f};
+      const float dsv[8] = {h ? 0.f : ds_hi, h ? 0.f : ds - ds_hi, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      const auto r8 = slab_rsrc<E>(a.d8, 32, wglob);
+      plane_store_oct<E>(r8, voff, 0, 0, d8v);
+      plane_store_oct<E>(r8, voff, 0, 1, z8);
+      const auto rv = slab_rsrc<E>(a.dA[SB + 2], 288, wglob);
+      plane_store_oct<E>(rv, voff, 8, 0, dsv);
+      plane_store_oct<E>(rv, voff, 8, 1, z8);
     }
     // ReLU sign bits of this wave -> LDS
-    const u32x4* src = (const u32x4*)a.masks + (size_t)wread * N::kMasks * 64 + lane;
     u32x4* dst = (u32x4*)(smem + kMaskOff) + (size_t)w * N::kMasks * 64 + lane;
 #pragma unroll
-    for (int k = 0; k < N::kMasks; ++k) dst[k * 64] = src[k * 64];
+    for (int k = 0; k < N::kMasks; ++k) dst[k * 64] = in.mw[k];
     return ds;
   }
 

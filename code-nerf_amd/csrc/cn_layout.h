@@ -179,20 +179,26 @@ inline constexpr int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 *
 // hh = (c >> 2) & 1) hits bank 4 ((s + g + 4 hh) mod 8) + (c & 3): all 32
 // banks (a rotation by 8 g put the four groups on the same 8 banks: 4-way).
 //
-// bf16 (16 B = 8 features): per 16-feature pair block gp, 64 positions of 8
-// consecutive features 16 gp + 8 gg .. +7; sample s sits at
-//     pos = 32 gg + ((s + 8 gp + 4 gg) & 31).
-// The chain epilogues exchange lane halves (v_permlane32_swap) so that lane
-// s + 32 gg holds exactly those 8 features and one 16-B store per lane fills a
-// whole 1 KiB pair block.  The rotation by 8 gp + 4 gg makes the dW kernel's
-// transposed LDS reads (ds_read_b64_tr_b16: 4 samples x 4 features per lane,
-// a 32-lane half spanning 4 samples x 32 features) hit 64 distinct banks.
+// bf16 (16 B = 8 features): per 16-feature pair block gp, 64 positions of 16
+// B; position hh (lane half) of sample s holds the two feature quads a lane
+// half hh owns after an MFMA (accumulator rows 4 hh .. +3 of both 8-row
+// groups): features 16 gp + 4 hh .. +3 in its first 8 bytes and
+// 16 gp + 8 + 4 hh .. +3 in its second, at
+//     pos = 32 hh + ((s + 8 gp + 4 hh) & 31).
+// So lane s + 32 hh stores its 8 features of a pair block as they sit in its
+// registers with ONE 16-B store, and one store instruction fills the whole
+// 1 KiB pair block (round 6; rounds 4-5: two 8-B stores per pair block, the
+// quads of one 8-feature group side by side; round 3: a v_permlane32_swap
+// lane exchange before a 16-B store).  The rotation by 8 gp + 4 hh makes the
+// dW kernel's transposed LDS reads (ds_read_b64_tr_b16: 4 samples x 4
+// features per lane, a 32-lane half spanning 4 samples x 32 features) hit 64
+// distinct banks: bank pair 4 ((s + 8 gp + 4 hh) mod 16) + 2 gg.
 inline constexpr int tile_pos(int s, int g, int hh) { return ((s + g + 4 * hh) & 31) + 32 * hh; }
-inline constexpr int bf16_pos(int s, int gp, int gg) { return 32 * gg + ((s + 8 * gp + 4 * gg) & 31); }
+inline constexpr int bf16_pos(int s, int gp, int hh) { return 32 * hh + ((s + 8 * gp + 4 * hh) & 31); }
 // byte offset, inside a 32-sample slab, of features f .. f+3 (f % 4 == 0) of sample s
 inline constexpr int slab_off(int s, int f, int es) {
-  return es == 2 ? (f >> 5) * 2048 + ((f >> 4) & 1) * 1024 + bf16_pos(s, (f >> 4) & 1, (f >> 3) & 1) * 16 +
-                       ((f >> 2) & 1) * 8
+  return es == 2 ? (f >> 5) * 2048 + ((f >> 4) & 1) * 1024 + bf16_pos(s, (f >> 4) & 1, (f >> 2) & 1) * 16 +
+                       ((f >> 3) & 1) * 8
                  : (f >> 5) * 4096 + ((f >> 3) & 3) * 1024 + tile_pos(s, (f >> 3) & 3, (f >> 2) & 1) * 16;
 }
 // byte offset of features f .. f+3 of sample m in a plane of width F

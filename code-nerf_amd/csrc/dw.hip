@@ -496,8 +496,8 @@ __global__ __launch_bounds__(256) void dw_fold_kernel(DwFoldArgs a) {
 // ---------------------------------------------------------------- bias only
 // Column sums of the 256-wide dA planes of the code-fed layers, streamed in
 // 16-B chunks: in a slab, thread t reads chunks t + 256 k, which always hold
-// the same sample's 8 (bf16) / 4 (fp32) consecutive features of tiles
-// advancing with k; each lane sums its sample over the workgroup's slabs, then
+// the same sample's 8 (bf16: two quads, cn_layout.h) / 4 (fp32) features of
+// tiles advancing with k; each lane sums its sample over the workgroup's slabs, then
 // the 32 lanes of a half-wave (the 32 samples) are combined by an xor tree.
 template <int P>
 __global__ __launch_bounds__(256) void db_kernel(DbArgs a) {
@@ -543,10 +543,13 @@ __global__ __launch_bounds__(256) void db_kernel(DbArgs a) {
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
       const int c = t + 256 * k;
-      const int f0 = kBf16 ? 32 * (c >> 7) + 16 * ((c >> 6) & 1) + 8 * ((c >> 5) & 1)
+      // bf16 chunk (tile, pair block gp, lane half hh): features 16 gp + 4 hh
+      // + (e & 3) + 8 (e >> 2); fp32 chunk: 4 consecutive features
+      const int f0 = kBf16 ? 32 * (c >> 7) + 16 * ((c >> 6) & 1) + 4 * ((c >> 5) & 1)
                            : 32 * (c >> 8) + 8 * ((c >> 6) & 3) + 4 * ((c >> 5) & 1);
 #pragma unroll
-      for (int e = 0; e < EPC; ++e) a.part[((size_t)j * kDbBlocks + blk) * 256 + f0 + e] = acc[k][e];
+      for (int e = 0; e < EPC; ++e)
+        a.part[((size_t)j * kDbBlocks + blk) * 256 + f0 + (kBf16 ? (e & 3) + 8 * (e >> 2) : e)] = acc[k][e];
     }
   }
 }

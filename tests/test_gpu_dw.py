@@ -65,10 +65,10 @@ def decode(act, off, F, Mp, dtype):
     f = torch.arange(F, device=dev)[None, :]
     s = m & 31
     slab = (m >> 5) * (F * 32) + (f >> 5) * 1024
-    if es == 2:     # 16-feature pair blocks of 64 x 8 elements
-        gp, gg = (f >> 4) & 1, (f >> 3) & 1
-        pos = 32 * gg + ((s + 8 * gp + 4 * gg) & 31)
-        elem = slab + gp * 512 + pos * 8 + (f & 7)
+    if es == 2:     # 16-feature pair blocks of 64 x 8 elements: position hh holds quads 4hh and 8 + 4hh
+        gp, gg, hh = (f >> 4) & 1, (f >> 3) & 1, (f >> 2) & 1
+        pos = 32 * hh + ((s + 8 * gp + 4 * hh) & 31)
+        elem = slab + gp * 512 + pos * 8 + gg * 4 + (f & 3)
     else:           # 8-feature groups of 64 x 4 elements
         g, hh = (f >> 3) & 3, (f >> 2) & 1
         pos = ((s + g + 4 * hh) & 31) + 32 * hh

@@ -48,13 +48,14 @@ def _pe_slot_feature(h, s):
 def _decode(buf, off, F, M):
     """bf16 plane of width F at byte offset ``off`` -> (M, F) float32
     (cn_layout.h: slab of 32 samples = F/32 tiles of two 1 KiB pair blocks;
-    sample s, features 16gp + 8gg .. +7 at position 32gg + ((s + 8gp + 4gg) & 31))."""
+    sample s, features 16gp + 4hh .. +3 and 16gp + 8 + 4hh .. +3 at position
+    32hh + ((s + 8gp + 4hh) & 31), in its first and second 8 bytes)."""
     m = np.arange(M)[:, None]
     f = np.arange(F)[None, :]
     s = m & 31
-    gp, gg = (f >> 4) & 1, (f >> 3) & 1
-    pos = 32 * gg + ((s + 8 * gp + 4 * gg) & 31)
-    byte = (m >> 5) * F * 64 + (f >> 5) * 2048 + gp * 1024 + pos * 16 + ((f >> 2) & 1) * 8 + (f & 3) * 2
+    gp, gg, hh = (f >> 4) & 1, (f >> 3) & 1, (f >> 2) & 1
+    pos = 32 * hh + ((s + 8 * gp + 4 * hh) & 31)
+    byte = (m >> 5) * F * 64 + (f >> 5) * 2048 + gp * 1024 + pos * 16 + gg * 8 + (f & 3) * 2
     raw = buf[off:].view(torch.int16).cpu().numpy()
     vals = raw[(byte // 2).reshape(-1)].reshape(M, F).astype(np.int32) << 16
     return torch.from_numpy(vals.view(np.float32).copy())
