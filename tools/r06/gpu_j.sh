@@ -3,7 +3,7 @@
 # early-issue and spread changes alter every rounding order, so the chaotic
 # trajectories are re-run, not assumed).
 export TMPDIR=/tmp
-OUT=gpurun_out/r06j
+OUT=gpurun_out/${TAG:-r06j}
 mkdir -p $OUT
 timeout -k 10 1150 python -u -m pytest -v -rA --timeout 1100 --timeout-method thread tests/test_gpu_regime.py \
   tests/test_gpu_regime_fine.py tests/test_gpu_converge.py > $OUT/pytest_psnr.log 2>&1
