@@ -582,7 +582,10 @@ def roofline(args, timers, samples_per_step, ms, overlapped, precision=None, ste
     if tr:
         alg_launch = alg_b * d["samples_per_launch"]
         roof["algorithmic"].update(hbm_bytes_per_launch=round(alg_launch),
-                                   counter_over_algorithmic_bytes=round(tr["hbm_bytes_per_launch"] / alg_launch, 1))
+                                   counter_over_algorithmic_bytes=round(tr["hbm_bytes_per_launch"] / alg_launch, 1),
+                                   note="the step's own I/O bytes (ray, gt, rgb); the training chains' counted "
+                                        "bytes are the activation planes the dW pass reads back (forward: "
+                                        "written, dX: read and written) and the weight stream")
     step_flops = sum(v for k, v in FLOP_PER_SAMPLE.items() if k in passes) * samples_per_step
     roof["step"] = {"achieved": round(step_flops / (ms * 1e-3) / 1e12, 2), "unit": "TFLOP/s",
                     "frac": round(step_flops / (ms * 1e-3) / 1e12 / peak, 4)}
