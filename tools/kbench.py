@@ -37,6 +37,9 @@ def main():
     ap.add_argument("--only", default="fwd,bwd,dw,copy")
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--dw-rows", default="", help="comma list of row counts: dW timed over rows [0, n) too")
+    ap.add_argument("--weight-scale", type=float, default=1.0,
+                    help="timing probe: scale every weight / code by this before timing (0: all-zero operands -- "
+                         "the matrix cores' data-dependent power)")
     a = ap.parse_args()
     only = set(a.only.split(","))
     from codenerf_amd.model import CodeNeRF
@@ -61,9 +64,13 @@ def main():
     with torch.no_grad():
         for p, q in zip(model.param_list() + [sc, tc], saved):
             p.copy_(q)
+        if a.weight_scale != 1.0:
+            for p in model.param_list() + [sc, tc]:
+                p.mul_(a.weight_scale)
     step = core.step_impl
     eng = model.engine()
     params = model.param_list()
+    eng.ensure_packed(params)
     Mc = R * 64
     M = eng.pad(Mc) + R * 64
     buf = step._ws[eng.device]
@@ -109,6 +116,7 @@ def main():
         out["read_GBs"] = round(x.numel() / t / 1e6, 1)
     out["lib"] = os.environ.get("CODENERF_LIB", "default")
     out["precision"] = a.precision
+    out["weight_scale"] = a.weight_scale
     print(json.dumps(out))
 
 

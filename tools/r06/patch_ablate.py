@@ -4,6 +4,8 @@
 #   abl_nobar   no LDS-DMA and no per-chunk barrier
 #   abl_noepi   no forward tile epilogue (conversion, ReLU, masks, bias, stores)
 #   abl_floor   no LDS-DMA, no barrier, no tile epilogue: MFMAs + A-fragment reads
+#   abl_nowait  the LDS-DMA issued, its counted vmcnt waits dropped (barriers kept)
+#   abl_bardma  the LDS-DMA and its waits, no per-chunk barrier
 import os
 import sys
 d = sys.argv[1]
@@ -26,6 +28,18 @@ if name in ("abl_nodma", "abl_nobar", "abl_floor"):
     sub("""  __device__ static void issue(const ChainArgs& a, char* smem, int w, int lane) {
 """, """  __device__ static void issue(const ChainArgs& a, char* smem, int w, int lane) {
     """ + X3)
+if name == "abl_nowait":
+    sub("""        wait_vmcnt<vm_wait(wc)>();
+        block_barrier_noread();
+""", """        if constexpr (!(kX3 && !BWD)) wait_vmcnt<vm_wait(wc)>();
+        block_barrier_noread();
+""")
+if name == "abl_bardma":
+    sub("""        wait_vmcnt<vm_wait(wc)>();
+        block_barrier_noread();
+""", """        wait_vmcnt<vm_wait(wc)>();
+        if constexpr (!(kX3 && !BWD)) block_barrier_noread();
+""")
 if name in ("abl_nobar", "abl_floor"):
     sub("""        wait_vmcnt<vm_wait(wc)>();
         block_barrier_noread();
