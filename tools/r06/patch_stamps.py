@@ -20,6 +20,15 @@ sub('''    const int lane = threadIdx.x & 63;
     '''    const uint64_t st0 = __builtin_amdgcn_s_memtime();
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);''')
+sub('''    BinT bin[kBin];
+    BinT binl[kX3 ? kBin : 1];     // bf16x3: the operand's lo parts''', '''    const uint64_t sta = __builtin_amdgcn_s_memtime();   // blob in LDS (its loads returned)
+    BinT bin[kBin];
+    BinT binl[kX3 ? kBin : 1];     // bf16x3: the operand's lo parts''')
+sub('''    __syncthreads();
+    if constexpr (!BWD) load_bias<0>(acc, prm, h);''', '''    const uint64_t stb = __builtin_amdgcn_s_memtime();   // prologue done (PE, its stores issued)
+    __syncthreads();
+    const uint64_t stc = __builtin_amdgcn_s_memtime();   // past the barrier
+    if constexpr (!BWD) load_bias<0>(acc, prm, h);''')
 sub('''    // (two nested loops: one static_for over ~300 blocks would exceed the
     // template instantiation depth)
     static_for<0, kChunks>([&](auto cc) {
@@ -46,6 +55,7 @@ sub('''    // (two nested loops: one static_for over ~300 blocks would exceed th
         uint32_t* o = (uint32_t*)a.sigma + (size_t)blockIdx.x * (WAVES * 32);
         o[0] = (uint32_t)st0; o[1] = (uint32_t)st1; o[2] = (uint32_t)st2;
         o[3] = hw; o[4] = xcc; o[5] = 0x57a3u;
+        o[6] = (uint32_t)sta; o[7] = (uint32_t)stb; o[8] = (uint32_t)stc;
       }
     }
   }''')

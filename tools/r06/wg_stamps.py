@@ -54,11 +54,14 @@ def main():
         eng.mlp_fwd(blob, Mc, rays_o=ro, rays_d=vd, z=z, n_samples=64, act=buf["act"], act_M=buf["cap"],
                     act_row0=0, sigma=sig, rgb=buf["rgb"][:eng.pad(Mc)])
     torch.cuda.synchronize()
-    st = sig.view(torch.int32).view(-1, 128)[:, :6].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+    st = sig.view(torch.int32).view(-1, 128)[:, :9].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
     assert (st[:, 5] == 0x57A3).all(), "not the stamps variant"
     t0, t1, t2 = st[:, 0], st[:, 1], st[:, 2]
     base = t0.min()
     t0, t1, t2 = (t0 - base) % 2**32, (t1 - base) % 2**32, (t2 - base) % 2**32
+    ta, tb, tc = ((st[:, k] - base) % 2**32 for k in (6, 7, 8))
+    phases = {"entry_to_blob_in_lds": float(np.mean(ta - t0)), "prologue_pe_and_stores": float(np.mean(tb - ta)),
+              "barrier": float(np.mean(tc - tb)), "to_first_block": float(np.mean(t1 - tc))}
     hw, xcc = st[:, 3], st[:, 4]
     # CU identity: XCC id, and HW_ID's SE (bits 13-15), SH (12), CU (8-11)
     cu = xcc * 1000 + ((hw >> 13) & 7) * 100 + ((hw >> 12) & 1) * 20 + ((hw >> 8) & 15)
@@ -78,7 +81,7 @@ def main():
                 gap += a - v[k - 1][2]
     out = {"workgroups": int(len(t0)), "cus": len(per), "wg_per_cu": [int(min(nwg)), int(max(nwg))],
            "wg_cycles_mean": float(np.mean(t2 - t0)), "prologue_cycles_mean": float(np.mean(t1 - t0)),
-           "body_cycles_mean": float(np.mean(t2 - t1)),
+           "body_cycles_mean": float(np.mean(t2 - t1)), "prologue_phases_cycles": phases,
            "share_of_cu_span": {"prologue": round(pro / span, 4), "between_workgroups": round(gap / span, 4),
                                 "blocks": round(body / span, 4)}}
     print(json.dumps(out))
